@@ -1,0 +1,120 @@
+"""ctypes front-end of the two oracles -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+The product path (libptmi.so) never links or calls anything under oracle/.
+
+* ``ref_trace``  -- the reference kernel itself (tracer.cl compiled by ROCm's OpenCL
+  toolchain, oracle/_ref/tracer_ref.hsaco) dispatched on a GPU through HSA.
+* ``cpu_trace``  -- the C restatement of the same algorithm (oracle/pt_oracle.c,
+  oracle/build/libptoracle.so), multithreaded with OpenMP.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF_HSACO = os.path.join(HERE, "_ref", "tracer_ref.hsaco")
+REF_LIB = os.path.join(HERE, "_ref", "libptref.so")
+CPU_LIB = os.path.join(HERE, "build", "libptoracle.so")
+
+_ref = None
+_cpu = None
+
+
+def ref_available():
+    return os.path.exists(REF_HSACO) and os.path.exists(REF_LIB) and os.path.exists(REF_HSACO + ".args")
+
+
+def _as_bytes_ptr(a):
+    a = np.ascontiguousarray(a)
+    return a, a.ctypes.data_as(ctypes.c_void_p)
+
+
+def ref_trace(objects, triangles, groups, camera, samples, seeds, device_index=0, wg_size=None,
+              timeout_s=600.0):
+    """Run the reference OpenCL kernel on the GPU; returns float64 RGBA [H*W*4]."""
+    global _ref
+    if _ref is None:
+        _ref = ctypes.CDLL(REF_LIB)
+        _ref.ptref_trace.restype = ctypes.c_int
+        _ref.ptref_trace.argtypes = [ctypes.c_char_p, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                     ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                     ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                     ctypes.c_double, ctypes.c_char_p, ctypes.c_size_t]
+    cam = np.asarray(camera).reshape(())
+    w, h = int(cam["width"]), int(cam["height"])
+    n = w * h
+    if wg_size is None:
+        wg_size = next(g for g in (256, 128, 64, 32, 16, 8, 4, 2, 1) if n % g == 0)
+    seeds = np.ascontiguousarray(seeds, dtype=np.float64)
+    assert seeds.size == n
+    out = np.zeros(n * 4, dtype=np.float64)
+    objects, po = _as_bytes_ptr(objects)
+    triangles, pt = _as_bytes_ptr(triangles)
+    groups, pg = _as_bytes_ptr(groups)
+    cam_arr, pc = _as_bytes_ptr(cam)
+    err = ctypes.create_string_buffer(512)
+    rc = _ref.ptref_trace(REF_HSACO.encode(), device_index, po, len(objects), pt, len(triangles),
+                          pg, len(groups), pc, samples, seeds.ctypes.data_as(ctypes.c_void_p), n,
+                          wg_size, out.ctypes.data_as(ctypes.c_void_p), timeout_s, err, len(err))
+    if rc != 0:
+        raise RuntimeError("ptref_trace rc=%d: %s" % (rc, err.value.decode(errors="replace")))
+    return out
+
+
+def cpu_available():
+    return os.path.exists(CPU_LIB)
+
+
+def _cpu_lib():
+    global _cpu
+    if _cpu is None:
+        _cpu = ctypes.CDLL(CPU_LIB)
+        _cpu.pto_trace.restype = ctypes.c_int
+        _cpu.pto_trace.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                   ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                   ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                   ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
+        _cpu.pto_noise3d.restype = ctypes.c_float
+        _cpu.pto_noise3d.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float]
+        _cpu.pto_sinf32.restype = ctypes.c_float
+        _cpu.pto_sinf32.argtypes = [ctypes.c_float]
+        _cpu.pto_sinf_many.restype = None
+        _cpu.pto_sinf_many.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    return _cpu
+
+
+def cpu_trace(objects, triangles, groups, camera, samples, seeds, row0=0, rows=None,
+              sample_begin=0, sample_end=None, threads=0):
+    """C restatement of the reference kernel.  Returns float64 RGBA for rows
+    [row0, row0+rows).  ``sample_begin/end`` select a sub-range of the S samples
+    (global indices, as a multi-GPU sample split passes them); with a partial
+    range the result is the un-normalised sum (like one GPU's partial frame)."""
+    lib = _cpu_lib()
+    cam = np.asarray(camera).reshape(())
+    w, h = int(cam["width"]), int(cam["height"])
+    rows = h - row0 if rows is None else rows
+    sample_end = samples if sample_end is None else sample_end
+    seeds = np.ascontiguousarray(seeds, dtype=np.float64)
+    assert seeds.size == w * h
+    out = np.zeros(w * rows * 4, dtype=np.float64)
+    objects, po = _as_bytes_ptr(objects)
+    triangles, pt = _as_bytes_ptr(triangles)
+    groups, pg = _as_bytes_ptr(groups)
+    cam_arr, pc = _as_bytes_ptr(cam)
+    rc = lib.pto_trace(po, len(objects), pt, len(triangles), pg, len(groups), pc, samples,
+                       seeds.ctypes.data_as(ctypes.c_void_p), row0, rows, sample_begin, sample_end,
+                       threads, out.ctypes.data_as(ctypes.c_void_p))
+    if rc != 0:
+        raise RuntimeError("pto_trace rc=%d" % rc)
+    return out
+
+
+def noise3d(x, y, z):
+    return _cpu_lib().pto_noise3d(x, y, z)
+
+
+def sinf(x):
+    return _cpu_lib().pto_sinf32(x)

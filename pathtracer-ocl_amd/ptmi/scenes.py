@@ -1,0 +1,248 @@
+"""Restatement of the reference's camera (internal/app/camera/camera.go) and of the
+scene factories the benchmark configs use:
+
+* ``reference``  scenes/reference.go:12-83   (configs C1-C3)
+* ``teapot``     scenes/teapot.go:15-125     (config C4, ModelScene)
+* ``gopher``     scenes/gopher.go            (config C5)
+* ``default``    scenes/ocl.go               (OCLScene: every primitive type, glass, mirror)
+
+Go untyped constants (``math.Pi/3`` ...) are rounded ONCE to float64, unlike
+Python's ``math.pi/3`` which rounds twice; they are spelled out below.
+"""
+import math
+import os
+
+from . import geom, objparser, shapes
+from .gomath import Tan
+
+PI_OVER_2 = 1.5707963267948966    # float64(math.Pi / 2)
+PI_OVER_3 = 1.0471975511965979    # float64(math.Pi / 3)  (!= math.pi / 3)
+PI_OVER_4 = 0.7853981633974483    # float64(math.Pi / 4)
+
+# The OBJ/MTL assets are read from the reference checkout (this container only);
+# the GPU box uses the scene records pre-built from them (tests/golden/scene_*.npz,
+# made by tests/golden/make_scenes.py).
+ASSETS = os.environ.get("PTMI_ASSETS", "/root/reference/assets")
+
+
+class Camera:
+    """camera.Camera (camera.go:8-19)."""
+
+    def __init__(self, width, height, fov, frm, to):
+        half_view = Tan(fov / 2)
+        aspect = float(width) / float(height)
+        if aspect >= 1.0:
+            half_width = half_view
+            half_height = half_view / aspect
+        else:
+            half_width = half_view * aspect
+            half_height = half_view
+        self.width = int(width)
+        self.height = int(height)
+        self.fov = fov
+        self.pixel_size = (half_width * 2) / float(width)
+        self.transform = view_transform(frm, to, geom.vector(0, 1, 0))
+        self.inverse = geom.inverse(self.transform)
+        self.half_width = half_width
+        self.half_height = half_height
+        self.aperture = 0.0
+        self.focal_length = 0.0
+
+
+def view_transform(frm, to, up):
+    """camera.ViewTransform (camera.go:50-81)."""
+    vt = geom.identity()
+    forward = geom.normalize(geom.sub(to, frm))
+    up_n = geom.normalize(up)
+    left = geom.cross(forward, up_n)
+    true_up = geom.cross(left, forward)
+    vt[0], vt[1], vt[2] = left[0], left[1], left[2]
+    vt[4], vt[5], vt[6] = true_up[0], true_up[1], true_up[2]
+    vt[8], vt[9], vt[10] = -forward[0], -forward[1], -forward[2]
+    return geom.multiply(vt, geom.translate(-frm[0], -frm[1], -frm[2]))
+
+
+class Scene:
+    def __init__(self, camera, objects):
+        self.camera = camera
+        self.objects = objects
+
+
+def _std_camera(width, height, aperture, focal_length):
+    cam = Camera(width, height, PI_OVER_3, geom.point(0, 0.1, -1.5), geom.point(0, 0.05, 0))
+    cam.focal_length = float(focal_length)
+    cam.aperture = float(aperture)
+    return cam
+
+
+def _walls(back_z=.4):
+    left = shapes.Plane()
+    left.set_transform(geom.translate(-.6, 0, 0))
+    left.set_transform(geom.rotate_z(PI_OVER_2))
+    left.set_material(shapes.new_diffuse(0.75, 0.25, 0.25))
+    right = shapes.Plane()
+    right.set_transform(geom.translate(.6, 0, 0))
+    right.set_transform(geom.rotate_z(PI_OVER_2))
+    right.set_material(shapes.new_diffuse(0.25, 0.25, 0.75))
+    floor = shapes.Plane()
+    floor.set_transform(geom.translate(0, -.4, 0))
+    floor.set_material(shapes.new_diffuse(0.9, 0.8, 0.7))
+    ceil = shapes.Plane()
+    ceil.set_transform(geom.translate(0, .4, 0))
+    ceil.set_material(shapes.new_diffuse(0.9, 0.8, 0.7))
+    back = shapes.Plane()
+    back.set_transform(geom.translate(0, 0, back_z))
+    back.set_transform(geom.rotate_x(PI_OVER_2))
+    back.set_material(shapes.new_diffuse(0.9, 0.8, 0.7))
+    front = shapes.Plane()
+    front.set_transform(geom.translate(0, 0, -2))
+    front.set_transform(geom.rotate_x(PI_OVER_2))
+    front.set_material(shapes.new_diffuse(0.9, 0.8, 0.7))
+    return left, right, floor, ceil, back, front
+
+
+def reference_scene(width, height, aperture=0.0, focal_length=0.0):
+    """ReferenceScene (scenes/reference.go:12-83): the Cornell box with two diffuse
+    spheres; the front wall is built but not added (reference.go:76)."""
+    cam = _std_camera(width, height, aperture, focal_length)
+    left, right, floor, ceil, back, _front = _walls()
+    ls = shapes.Sphere()
+    ls.set_transform(geom.translate(-0.35, -0.28, -0.15))
+    ls.set_transform(geom.scale(0.12, 0.12, 0.12))
+    ls.set_material(shapes.new_diffuse(0.9, 0.8, 0.7))
+    rs = shapes.Sphere()
+    rs.set_transform(geom.translate(0, -0.24, -0.30))
+    rs.set_transform(geom.scale(0.16, 0.16, 0.16))
+    rs.set_material(shapes.new_diffuse(0.9, 0.8, 0.7))
+    light_src = shapes.Sphere()
+    light_src.set_transform(geom.translate(0, .399, 0))
+    light_src.set_transform(geom.scale(0.283, 0.01, 0.283))
+    light = shapes.new_light_bulb()
+    light.emission = geom.color(9, 9, 9)
+    light_src.set_material(light)
+    return Scene(cam, [light_src, floor, ceil, left, right, back, ls, rs])
+
+
+def ocl_scene(width, height, aperture=0.0, focal_length=0.0):
+    """OCLScene (scenes/ocl.go), the CLI default: planes, diffuse / glass / mirror
+    spheres, cylinder, cube and a 3-triangle group (which has no sub-groups, so
+    BuildSceneBufferCL gives it childCount 0 and the kernel never tests it)."""
+    cam = _std_camera(width, height, aperture, focal_length)
+    left, right, floor, ceil, back, _front = _walls()
+    lsp = shapes.Sphere()
+    lsp.set_transform(geom.translate(-0.25, -0.24, 0.1))
+    lsp.set_transform(geom.scale(0.16, 0.16, 0.16))
+    lsp.set_material(shapes.new_diffuse(0.9, 0.8, 0.7))
+    msp = shapes.Sphere()
+    msp.set_transform(geom.translate(0, -0.24, -0.30))
+    msp.set_transform(geom.scale(0.16, 0.16, 0.16))
+    msp.set_material(shapes.new_glass())
+    rsp = shapes.Sphere()
+    rsp.set_transform(geom.translate(0.25, -0.24, 0.1))
+    rsp.set_transform(geom.scale(0.16, 0.16, 0.16))
+    half_mirror = shapes.new_mirror()
+    half_mirror.reflectivity = 0.8
+    half_mirror.color = geom.color(0.97, 0.97, 0.843)
+    rsp.set_material(half_mirror)
+    cyl = shapes.Cylinder(0, 0.4, True)
+    cyl.set_transform(geom.translate(0.45, -0.5, -0.2))
+    cyl.set_transform(geom.scale(0.075, 1, 0.075))
+    cyl.set_material(shapes.new_diffuse(0.92, 0.4, 0.8))
+    cube = shapes.Cube()
+    cube.set_transform(geom.translate(-0.3, -0.375, -0.3))
+    cube.set_transform(geom.scale(0.1, 0.05, 0.04))
+    cube.set_transform(geom.rotate_y(PI_OVER_4))
+    cube.set_transform(geom.rotate_z(PI_OVER_2))
+    cube.set_material(shapes.new_diffuse(0.25, 0.25, 0.75))
+    light_src = shapes.Sphere()
+    light_src.set_transform(geom.translate(0, 1.36, 0))
+    light = shapes.new_light_bulb()
+    light.emission = geom.color(9, 8, 6)
+    light_src.set_material(light)
+    t1 = shapes.new_triangle_n(geom.point(-0.2, -.4, 0), geom.point(0.0, -.4, 0), geom.point(0, -0.1, 0))
+    t2 = shapes.new_triangle_n(geom.point(0, -.4, 0), geom.point(0.2, -.4, 0), geom.point(0, -0.1, 0))
+    t3 = shapes.new_triangle_n(geom.point(0.1, -.4, -0.4), geom.point(0, -0.1, 0), geom.point(0, -.4, 0))
+    grp = shapes.Group()
+    grp.set_material(shapes.new_diffuse(0.7, 0.4, 0.9))
+    grp.set_transform(geom.translate(0.15, 0, -0.25))
+    grp.add_children([t1, t2, t3])
+    grp.bounds()
+    return Scene(cam, [floor, ceil, left, right, back, lsp, rsp, cyl, cube, grp, light_src])
+
+
+def _load_obj(name):
+    path = os.path.join(ASSETS, name)
+    with open(path) as f:
+        return objparser.parse_obj(f.read(), base_dir=os.path.dirname(path))
+
+
+def teapot_scene(width, height, aperture=0.0, focal_length=0.0, obj_path=None):
+    """ModelScene (scenes/teapot.go:15-125): Cornell box + BVH teapot (Divide 50)."""
+    shapes.reset_subgroup_counter()
+    cam = _std_camera(width, height, aperture, focal_length)
+    left, right, floor, ceil, back, _front = _walls()
+    lsp = shapes.Sphere()
+    lsp.set_transform(geom.translate(-0.35, -0.28, -0.15))
+    lsp.set_transform(geom.scale(0.12, 0.12, 0.12))
+    lsp.set_material(shapes.new_diffuse(0.9, 0.8, 0.7))
+    model = _load_obj("teapot.obj") if obj_path is None else objparser.parse_obj(open(obj_path).read())
+    group = model.to_group()
+    tris = list(group.children[0].children)
+    objparser.compute_vertex_normals(tris)
+    group.bounds()
+    group.set_transform(geom.translate(0, -0.4, 0))
+    group.set_transform(geom.scale(0.07, 0.07, 0.07))
+    silver = shapes.new_diffuse(0.75, 0.75, 0.75)
+    silver.reflectivity = 0.2
+    group.set_material(silver)
+    shapes.divide(group, 50)
+    group.bounds()
+    light_src = shapes.Sphere()
+    light_src.set_transform(geom.translate(0, .4, 0))
+    light_src.set_transform(geom.scale(0.3, 0.03, 0.3))
+    light = shapes.new_light_bulb()
+    light.emission = geom.color(9, 8, 6)
+    light_src.set_material(light)
+    return Scene(cam, [light_src, floor, ceil, left, right, back, group, lsp])
+
+
+def gopher_scene(width, height, aperture=0.0, focal_length=0.0):
+    """GopherScene (scenes/gopher.go): Cornell box + BVH gopher (Divide 60)."""
+    shapes.reset_subgroup_counter()
+    cam = _std_camera(width, height, aperture, focal_length)
+    left, right, floor, ceil, back, front = _walls(back_z=1.4)
+    rsp = shapes.Sphere()
+    rsp.set_transform(geom.translate(0.28, -0.24, 0.15))
+    rsp.set_transform(geom.scale(0.16, 0.16, 0.16))
+    half_mirror = shapes.new_mirror()
+    half_mirror.reflectivity = 0.8
+    half_mirror.color = geom.color(0.97, 0.97, 0.843)
+    rsp.set_material(half_mirror)
+    objects = [floor, ceil, left, right, back, front, rsp]
+    group = _load_obj("gopher.obj").to_group()
+    group.bounds()
+    group.set_transform(geom.translate(-.4, -0.15, 0.2))
+    group.set_transform(geom.rotate_z(-PI_OVER_2))
+    group.set_transform(geom.rotate_x(-PI_OVER_4))
+    group.set_transform(geom.scale(0.2, 0.2, 0.2))
+    silver = shapes.new_diffuse(0.75, 0.75, 0.75)
+    silver.reflectivity = 0.2
+    group.set_material(silver)
+    shapes.divide(group, 60)
+    group.bounds()
+    objects.append(group)
+    light_src = shapes.Sphere()
+    light_src.set_transform(geom.translate(0, 1.36, 0))
+    light = shapes.new_light_bulb()
+    light.emission = geom.color(9, 8, 6)
+    light_src.set_material(light)
+    objects.append(light_src)
+    return Scene(cam, objects)
+
+
+SCENES = {
+    "reference": reference_scene,
+    "teapot": teapot_scene,
+    "gopher": gopher_scene,
+    "default": ocl_scene,
+}

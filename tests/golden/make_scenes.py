@@ -1,0 +1,34 @@
+"""Generate the committed BVH scene records (inputs, not reference code).
+
+The teapot / gopher scenes are built by ptmi's restatement of the reference's OBJ
+parser + BVH build from the OBJ assets in the reference checkout
+(/root/reference/assets, this container only).  The resulting kernel input
+records (CLObject / CLTriangle / CLGroup bytes, layout.py) are saved so tests and
+bench.py on the GPU box -- where /root/reference does not exist -- use the same
+inputs.  The camera record is not stored: it depends only on W/H/aperture/focal and
+is rebuilt by ``ptmi.scenes`` at run time.
+
+    python tests/golden/make_scenes.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "pathtracer-ocl_amd"))
+from ptmi import layout, scenes  # noqa: E402
+
+
+def main():
+    for name in ("teapot", "gopher"):
+        sc = scenes.SCENES[name](64, 48)
+        objs, tris, grps = layout.build_scene_buffer_cl(sc.objects)
+        out = os.path.join(HERE, "scene_%s.npz" % name)
+        np.savez_compressed(out, objects=objs.view(np.uint8), triangles=tris.view(np.uint8),
+                            groups=grps.view(np.uint8))
+        print(out, os.path.getsize(out), len(objs), len(tris), len(grps))
+
+
+if __name__ == "__main__":
+    main()
