@@ -1,0 +1,132 @@
+/*
+ * ptmi.h -- C ABI of libptmi.so, the MI355X (gfx950) path-tracing backend that
+ * replaces the reference's OpenCL host driver + kernel
+ * (eriklupander/pathtracer-ocl  internal/ocl/ocltracer.go + internal/ocl/tracer.cl).
+ *
+ * The input records are consumed BYTE-FOR-BYTE in the reference's packed layouts:
+ *   objects   : n_obj * 1024 B  CLObject   (ocltracer.go:25-51  == tracer.cl:37-63)
+ *   triangles : n_tri *  512 B  CLTriangle (ocltracer.go:66-78  == tracer.cl:82-93)
+ *   groups    : n_grp *  256 B  CLGroup    (ocltracer.go:53-64  == tracer.cl:24-35)
+ *   camera    :          256 B  CLCamera   (ocltracer.go:85-96  == tracer.cl:6-17)
+ * so a cgo caller passes &slice[0] of the slices BuildSceneBufferCL returns
+ * (see INTEGRATION.md).  No pointer is retained after a call returns.
+ *
+ * Output: float64 RGBA, row-major, W*H*4 values, RGB = sum of samples / samples,
+ * A = 1.0 (tracer.cl:1184-1187).
+ *
+ * Every entry point returns PTMI_OK (0) or a negative PTMI_ERR_* code and, when
+ * `err` is non-NULL, a NUL-terminated message.  There is no silent fallback:
+ * without a usable gfx950 device the calls fail.
+ */
+#ifndef PTMI_H
+#define PTMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PTMI_ABI_VERSION 1
+#define PTMI_OBJECT_BYTES 1024
+#define PTMI_TRIANGLE_BYTES 512
+#define PTMI_GROUP_BYTES 256
+#define PTMI_CAMERA_BYTES 256
+#define PTMI_MAX_OBJECTS 16 /* tracer.cl:846 `__local object objects[16]` */
+
+enum {
+    PTMI_OK = 0,
+    PTMI_ERR_ARG = -1,         /* bad sizes / NULL pointers / out-of-range indices   */
+    PTMI_ERR_DEVICE = -2,      /* no such device, or not a gfx950 device            */
+    PTMI_ERR_HIP = -3,         /* a HIP runtime call failed                          */
+    PTMI_ERR_UNSUPPORTED = -4, /* textured objects (read_imagef) -- not in this build */
+    PTMI_ERR_NOMEM = -5
+};
+
+/* Texture arrays of ocl.Trace (textures / sphereTextures / cubeTextures: NRGBA8
+ * image2d_array, ocltracer.go:228-254).  Reserved: must be NULL, or all counts 0;
+ * scenes with textured objects are rejected with PTMI_ERR_UNSUPPORTED. */
+typedef struct ptmi_textures {
+    const uint8_t* pixels[3];
+    uint32_t width[3], height[3], count[3];
+} ptmi_textures;
+
+/*
+ * ptmi_trace -- drop-in for `func Trace(objects []CLObject, triangles []CLTriangle,
+ *   groups []CLGroup, deviceIndex, samples int, camera CLCamera, textures,
+ *   sphereTextures, cubeTextures []image.Image) []float64`   (ocltracer.go:98-226).
+ *
+ *  - empty triangle / group slices are allowed (n = 0): the reference pads them
+ *    with one zero record (ocltracer.go:106-120), which is equivalent;
+ *  - device_index < 0 selects device 0 (ocltracer.go:138-140), an index past the
+ *    last device is an error (ocltracer.go:135-137: logrus.Fatalf);
+ *  - seeds: W*H per-pixel seeds in [0,1), row-major (the reference draws one
+ *    rand.Float64() per pixel, ocltracer.go:260-263).  NULL -> generated from
+ *    `seed_stream` (Go-Float64 granularity k/2^53, SplitMix64-derived);
+ *  - the frame is rendered in one resident launch sequence (the reference's 4-row
+ *    batches exist only to dodge a display watchdog, ocltracer.go:212-213).
+ */
+int ptmi_trace(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
+               const void* groups, uint32_t n_grp, int device_index, uint32_t samples,
+               const void* camera, const double* seeds, uint64_t seed_stream,
+               const ptmi_textures* textures, double* out_rgba, char* err, size_t err_len);
+
+/* --list-devices (cmd/pt/main.go:98-112). */
+int ptmi_device_count(void);
+int ptmi_device_name(int device_index, char* buf, size_t len);
+
+/* ------------------------------------------------------------------------
+ * Resident-scene API: the scene is converted and uploaded to HBM once, frames
+ * are rendered from device-resident seeds into device-resident sums on a
+ * caller-supplied HIP stream (hipStream_t passed as void*).  Used by bench.py,
+ * the multi-GPU driver and any caller that renders several frames / sample
+ * ranges per scene.  All device pointers are allocations on the scene's device.
+ * ------------------------------------------------------------------------ */
+typedef struct ptmi_scene ptmi_scene;
+
+int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, const void* triangles,
+                      uint32_t n_tri, const void* groups, uint32_t n_grp, const void* camera,
+                      ptmi_scene** out, char* err, size_t err_len);
+void ptmi_scene_destroy(ptmi_scene* s);
+int ptmi_scene_size(const ptmi_scene* s, uint32_t* width, uint32_t* height);
+
+/*
+ * Render samples [sample_begin, sample_end) of a `samples`-spp frame.
+ *   seeds_dev  : W*H doubles
+ *   sums_dev   : W*H*4 doubles, OVERWRITTEN with RGB sums over the sample range
+ *                (A = number of samples) for owned pixels, 0 for the others.
+ *   tile_stride/tile_offset: pixel ownership for a tile split -- 8x8 tile t is
+ *                owned when t % tile_stride == tile_offset (1/0 = all pixels).
+ *   chunks     : sample chunks per pixel (load balance; 0 = auto).  Chunk sums
+ *                are combined in a fixed order, so results are deterministic.
+ * Sample indices are GLOBAL (fgi2 = seed/samples and the DoF aperture pattern
+ * depend on n and on the total, tracer.cl:841, 766), so any split of
+ * [0, samples) sums to the same frame.
+ */
+int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, uint32_t sample_end,
+                      uint32_t tile_stride, uint32_t tile_offset, const double* seeds_dev,
+                      double* sums_dev, uint32_t chunks, void* hip_stream, char* err, size_t err_len);
+
+/* out_dev[i] = sums_dev[i] * (1.0 / samples) for RGB, 1.0 for A (tracer.cl:837,1184-1187). */
+int ptmi_finalize(const double* sums_dev, double* out_dev, uint32_t n_pixels, uint32_t samples,
+                  void* hip_stream, char* err, size_t err_len);
+
+/* Fill seeds_dev[0..n) with the generator ptmi_trace uses for seeds == NULL. */
+int ptmi_fill_seeds(double* seeds_dev, uint32_t n, uint64_t seed_stream, void* hip_stream, char* err,
+                    size_t err_len);
+
+/* Kernel timing: with timing enabled, every trace_kernel launch of the scene is
+ * bracketed by HIP events recorded on the launch stream; ptmi_scene_kernel_time
+ * waits for them, returns the summed kernel milliseconds and launch count since
+ * the last call, and resets the tally. */
+int ptmi_scene_set_timing(ptmi_scene* s, int enable);
+int ptmi_scene_kernel_time(ptmi_scene* s, double* total_ms, uint32_t* launches, char* err, size_t err_len);
+
+/* Build / ABI identification (kernel name, offload arch, flags). */
+const char* ptmi_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PTMI_H */

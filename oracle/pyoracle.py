@@ -36,6 +36,10 @@ def ref_trace(objects, triangles, groups, camera, samples, seeds, device_index=0
     """Run the reference OpenCL kernel on the GPU; returns float64 RGBA [H*W*4]."""
     global _ref
     if _ref is None:
+        try:  # share the process's HIP/HSA runtime with torch (see ptmi/_runtime.py)
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _ref = ctypes.CDLL(REF_LIB)
         _ref.ptref_trace.restype = ctypes.c_int
         _ref.ptref_trace.argtypes = [ctypes.c_char_p, ctypes.c_int,

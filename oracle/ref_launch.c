@@ -357,6 +357,8 @@ out:
     if (karg) hsa_amd_memory_pool_free(karg);
     if (printf_buf) hsa_amd_memory_pool_free(printf_buf);
     free(code);
-    if (inited) hsa_shut_down();
+    /* hsa_init() is reference counted; the runtime is left up (a HIP runtime in the
+     * same process shares it). */
+    (void)inited;
     return rc;
 }

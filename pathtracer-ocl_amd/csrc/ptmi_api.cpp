@@ -1,0 +1,464 @@
+// ptmi_api.cpp -- C ABI of libptmi.so (include/ptmi.h): record validation and
+// conversion to the HBM layout (ptmi_device.h), device residency, launch
+// orchestration.  Replaces the reference host driver internal/ocl/ocltracer.go
+// (Trace / computeBatch, ocltracer.go:98-376).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ptmi.h"
+#include "ptmi_device.h"
+
+namespace ptmi {
+hipError_t launch_trace(const DevScene& S, uint32_t samples, uint32_t s_begin, uint32_t s_end, uint32_t chunk_len,
+                        uint32_t nchunks, uint32_t tile_stride, uint32_t tile_offset, const double* seeds,
+                        double* out, hipStream_t st);
+hipError_t launch_reduce(const double* part, double* sums, uint32_t npix, uint32_t nchunks, int W, int H,
+                         uint32_t tile_stride, uint32_t tile_offset, hipStream_t st);
+hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint32_t samples, hipStream_t st);
+hipError_t launch_seeds(double* seeds, uint32_t n, uint64_t stream, hipStream_t st);
+const void* trace_kernel_symbol();
+}  // namespace ptmi
+
+using namespace ptmi;
+
+struct ptmi_scene {
+    int device = 0;
+    DevScene dev{};
+    void* buffers[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    double* partial = nullptr;  // chunk partial sums, grown on demand
+    size_t partial_bytes = 0;
+    int resident_waves = 0;  // device-wide resident waves of trace_kernel
+    uint32_t width = 0, height = 0;
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pending (start, stop) pairs
+    std::vector<hipEvent_t> spare;
+};
+
+namespace {
+
+void set_err(char* err, size_t n, const char* fmt, ...) {
+    if (!err || n == 0) return;
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(err, n, fmt, ap);
+    va_end(ap);
+}
+
+#define HIP_TRY(call)                                                                             \
+    do {                                                                                          \
+        hipError_t e_ = (call);                                                                   \
+        if (e_ != hipSuccess) {                                                                   \
+            set_err(err, err_len, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
+                    __LINE__);                                                                    \
+            return PTMI_ERR_HIP;                                                                  \
+        }                                                                                         \
+    } while (0)
+
+template <typename T>
+T rd(const uint8_t* p) {
+    T v;
+    std::memcpy(&v, p, sizeof(T));
+    return v;
+}
+
+int check_device(int idx, char* err, size_t err_len) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        set_err(err, err_len, "no HIP device available (ptmi requires an MI355X / gfx950)");
+        return PTMI_ERR_DEVICE;
+    }
+    if (idx < 0 || idx >= n) {
+        set_err(err, err_len, "device index %d out of bounds: highest device index: %d", idx, n - 1);
+        return PTMI_ERR_DEVICE;
+    }
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, idx) != hipSuccess) {
+        set_err(err, err_len, "hipGetDeviceProperties(%d) failed", idx);
+        return PTMI_ERR_DEVICE;
+    }
+    if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0) {
+        set_err(err, err_len, "device %d is %s; libptmi is built for gfx950 only", idx, p.gcnArchName);
+        return PTMI_ERR_DEVICE;
+    }
+    return PTMI_OK;
+}
+
+// Convert + validate the packed reference records (layout.py / tracer.cl:24-93).
+int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, uint32_t n_tri, const uint8_t* groups,
+                  uint32_t n_grp, const uint8_t* camera, std::vector<DevObject>& objs, std::vector<int32_t>& roots,
+                  std::vector<DevNode>& nodes, std::vector<DevTri>& ht, std::vector<DevTriShade>& st, DevCamera& cam,
+                  char* err, size_t err_len) {
+    if (!objects || n_obj == 0 || n_obj > PTMI_MAX_OBJECTS) {
+        set_err(err, err_len, "need 1..%d objects (tracer.cl:846 __local object objects[16]), got %u",
+                PTMI_MAX_OBJECTS, n_obj);
+        return PTMI_ERR_ARG;
+    }
+    if (!camera || (n_tri && !tris) || (n_grp && !groups)) {
+        set_err(err, err_len, "NULL record pointer");
+        return PTMI_ERR_ARG;
+    }
+    cam.width = rd<int32_t>(camera + 0);
+    cam.height = rd<int32_t>(camera + 4);
+    cam.pixel_size = rd<double>(camera + 16);
+    cam.half_width = rd<double>(camera + 24);
+    cam.half_height = rd<double>(camera + 32);
+    cam.aperture = rd<double>(camera + 40);
+    cam.focal_length = rd<double>(camera + 48);
+    std::memcpy(cam.inv, camera + 56, 128);
+    if (cam.width <= 0 || cam.height <= 0 || (int64_t)cam.width * cam.height > (int64_t)1 << 30) {
+        set_err(err, err_len, "bad camera size %dx%d", cam.width, cam.height);
+        return PTMI_ERR_ARG;
+    }
+    objs.resize(n_obj);
+    for (uint32_t i = 0; i < n_obj; i++) {
+        const uint8_t* b = objects + (size_t)PTMI_OBJECT_BYTES * i;
+        DevObject& o = objs[i];
+        std::memset(&o, 0, sizeof o);
+        std::memcpy(o.inv, b + 128, 128);
+        std::memcpy(o.inv_t, b + 256, 128);
+        std::memcpy(o.color, b + 384, 32);
+        std::memcpy(o.emission, b + 416, 32);
+        o.refractive_index = rd<double>(b + 448);
+        const int64_t type = rd<int64_t>(b + 456);
+        o.type = (type >= 0 && type <= 4) ? (int32_t)type : 999;
+        o.min_y = rd<double>(b + 464);
+        o.max_y = rd<double>(b + 472);
+        o.reflectivity = rd<double>(b + 480);
+        std::memcpy(o.bb_min, b + 520, 32);
+        std::memcpy(o.bb_max, b + 552, 32);
+        if (b[844] || b[846]) {
+            set_err(err, err_len,
+                    "object %u is textured (isTextured/isTexturedNM): read_imagef textures are not supported "
+                    "by this build",
+                    i);
+            return PTMI_ERR_UNSUPPORTED;
+        }
+        o.child_count = 0;
+        o.child_base = (int32_t)roots.size();
+        if (o.type == 4) {
+            const int32_t cc = rd<int32_t>(b + 584);
+            if (cc < 0 || cc > 64) {
+                set_err(err, err_len, "object %u: childCount %d out of range", i, cc);
+                return PTMI_ERR_ARG;
+            }
+            for (int32_t c = 0; c < cc; c++) {
+                const int32_t r = rd<int32_t>(b + 588 + 4 * c);
+                if (r < 0 || (uint32_t)r >= n_grp) {
+                    set_err(err, err_len, "object %u: child root %d outside %u groups", i, r, n_grp);
+                    return PTMI_ERR_ARG;
+                }
+                roots.push_back(r);
+            }
+            o.child_count = cc;
+        }
+    }
+    nodes.resize(n_grp);
+    for (uint32_t g = 0; g < n_grp; g++) {
+        const uint8_t* b = groups + (size_t)PTMI_GROUP_BYTES * g;
+        DevNode& n = nodes[g];
+        std::memcpy(n.bb_min, b + 0, 24);
+        std::memcpy(n.bb_max, b + 32, 24);
+        n.tri_offset = rd<int32_t>(b + 128);
+        n.tri_count = rd<int32_t>(b + 132);
+        n.child0 = rd<int32_t>(b + 140);
+        n.child1 = rd<int32_t>(b + 144);
+        if (n.tri_count < 0 || n.tri_offset < 0 || (int64_t)n.tri_offset + n.tri_count > (int64_t)n_tri ||
+            n.child0 >= (int32_t)n_grp || n.child1 >= (int32_t)n_grp) {
+            set_err(err, err_len, "group %u: triangle range [%d,+%d) / children (%d,%d) out of range", g,
+                    n.tri_offset, n.tri_count, n.child0, n.child1);
+            return PTMI_ERR_ARG;
+        }
+    }
+    ht.resize(n_tri);
+    st.resize(n_tri);
+    for (uint32_t t = 0; t < n_tri; t++) {
+        const uint8_t* b = tris + (size_t)PTMI_TRIANGLE_BYTES * t;
+        std::memcpy(ht[t].p1, b + 0, 32);
+        std::memcpy(ht[t].e1, b + 96, 32);
+        std::memcpy(ht[t].e2, b + 128, 32);
+        std::memcpy(st[t].n1, b + 160, 32);
+        std::memcpy(st[t].n2, b + 192, 32);
+        std::memcpy(st[t].n3, b + 224, 32);
+        std::memcpy(st[t].color, b + 256, 32);
+    }
+    return PTMI_OK;
+}
+
+template <typename T>
+int upload(const std::vector<T>& v, void** dst, char* err, size_t err_len) {
+    const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 256);
+    HIP_TRY(hipMalloc(dst, bytes));
+    if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return PTMI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ptmi_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int ptmi_device_name(int device_index, char* buf, size_t len) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device_index) != hipSuccess) return PTMI_ERR_DEVICE;
+    if (buf && len) snprintf(buf, len, "%s (%s, %d CUs)", p.name, p.gcnArchName, p.multiProcessorCount);
+    return PTMI_OK;
+}
+
+const char* ptmi_build_info(void) {
+    return "ptmi abi=1 arch=gfx950 fp=fp64 contract=off kernels=trace_kernel,reduce_chunks_kernel,finalize_kernel";
+}
+
+int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
+                      const void* groups, uint32_t n_grp, const void* camera, ptmi_scene** out, char* err,
+                      size_t err_len) {
+    if (!out) {
+        set_err(err, err_len, "out == NULL");
+        return PTMI_ERR_ARG;
+    }
+    *out = nullptr;
+    if (device_index < 0) device_index = 0;  // ocltracer.go:138-140
+    int rc = check_device(device_index, err, err_len);
+    if (rc) return rc;
+    std::vector<DevObject> objs;
+    std::vector<int32_t> roots;
+    std::vector<DevNode> nodes;
+    std::vector<DevTri> ht;
+    std::vector<DevTriShade> st;
+    DevCamera cam{};
+    rc = convert_scene((const uint8_t*)objects, n_obj, (const uint8_t*)triangles, n_tri, (const uint8_t*)groups, n_grp,
+                       (const uint8_t*)camera, objs, roots, nodes, ht, st, cam, err, err_len);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(device_index));
+    ptmi_scene* s = new ptmi_scene();
+    s->device = device_index;
+    s->width = (uint32_t)cam.width;
+    s->height = (uint32_t)cam.height;
+    if ((rc = upload(objs, &s->buffers[0], err, err_len)) || (rc = upload(roots, &s->buffers[1], err, err_len)) ||
+        (rc = upload(nodes, &s->buffers[2], err, err_len)) || (rc = upload(ht, &s->buffers[3], err, err_len)) ||
+        (rc = upload(st, &s->buffers[4], err, err_len))) {
+        ptmi_scene_destroy(s);
+        return rc;
+    }
+    s->dev.objs = (const DevObject*)s->buffers[0];
+    s->dev.roots = (const int32_t*)s->buffers[1];
+    s->dev.nodes = (const DevNode*)s->buffers[2];
+    s->dev.tris = (const DevTri*)s->buffers[3];
+    s->dev.tri_shade = (const DevTriShade*)s->buffers[4];
+    s->dev.n_obj = n_obj;
+    s->dev.n_nodes = n_grp;
+    s->dev.n_tri = n_tri;
+    s->dev.cam = cam;
+    hipDeviceProp_t p;
+    HIP_TRY(hipGetDeviceProperties(&p, device_index));
+    s->resident_waves = p.multiProcessorCount * 16;  // refined below from the occupancy query
+    int blocks_per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, trace_kernel_symbol(), 256, 0) ==
+            hipSuccess &&
+        blocks_per_cu > 0)
+        s->resident_waves = p.multiProcessorCount * blocks_per_cu * kWavesPerBlock;
+    *out = s;
+    return PTMI_OK;
+}
+
+void ptmi_scene_destroy(ptmi_scene* s) {
+    if (!s) return;
+    hipSetDevice(s->device);
+    for (void* b : s->buffers)
+        if (b) hipFree(b);
+    if (s->partial) hipFree(s->partial);
+    for (auto& e : s->events) {
+        hipEventDestroy(e.first);
+        hipEventDestroy(e.second);
+    }
+    for (auto e : s->spare) hipEventDestroy(e);
+    delete s;
+}
+
+int ptmi_scene_size(const ptmi_scene* s, uint32_t* w, uint32_t* h) {
+    if (!s) return PTMI_ERR_ARG;
+    if (w) *w = s->width;
+    if (h) *h = s->height;
+    return PTMI_OK;
+}
+
+int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, uint32_t sample_end,
+                      uint32_t tile_stride, uint32_t tile_offset, const double* seeds_dev, double* sums_dev,
+                      uint32_t chunks, void* hip_stream, char* err, size_t err_len) {
+    if (!s || !seeds_dev || !sums_dev || samples == 0 || sample_begin > sample_end || sample_end > samples ||
+        tile_stride == 0 || tile_offset >= tile_stride) {
+        set_err(err, err_len, "bad render arguments (samples %u range [%u,%u) tiles %u/%u)", samples, sample_begin,
+                sample_end, tile_offset, tile_stride);
+        return PTMI_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = (hipStream_t)hip_stream;
+    const uint32_t W = s->width, H = s->height, npix = W * H;
+    const uint32_t range = sample_end - sample_begin;
+    const uint32_t tiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+    const uint32_t owned_tiles = (tiles + tile_stride - 1 - tile_offset) / tile_stride;
+    if (chunks == 0) {
+        // Enough waves for ~8 per resident slot (tail balance), >= 16 samples per chunk.
+        const uint64_t want = (uint64_t)s->resident_waves * 8;
+        chunks = (uint32_t)std::min<uint64_t>((want + owned_tiles - 1) / std::max<uint32_t>(owned_tiles, 1),
+                                              std::max<uint32_t>(range / 16, 1));
+    }
+    chunks = std::max<uint32_t>(1, std::min<uint32_t>(chunks, std::max<uint32_t>(range, 1)));
+    const uint32_t chunk_len = range == 0 ? 1 : (range + chunks - 1) / chunks;
+    chunks = range == 0 ? 1 : (range + chunk_len - 1) / chunk_len;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (s->timing) {
+        for (hipEvent_t* e : {&ev0, &ev1}) {
+            if (!s->spare.empty()) {
+                *e = s->spare.back();
+                s->spare.pop_back();
+            } else {
+                HIP_TRY(hipEventCreate(e));
+            }
+        }
+    }
+    if (chunks == 1) {
+        if (tile_stride > 1) HIP_TRY(hipMemsetAsync(sums_dev, 0, (size_t)npix * 4 * sizeof(double), st));
+        if (ev0) HIP_TRY(hipEventRecord(ev0, st));
+        HIP_TRY(launch_trace(s->dev, samples, sample_begin, sample_end, chunk_len, 1, tile_stride, tile_offset,
+                             seeds_dev, sums_dev, st));
+        if (ev1) {
+            HIP_TRY(hipEventRecord(ev1, st));
+            s->events.emplace_back(ev0, ev1);
+        }
+        return PTMI_OK;
+    }
+    const size_t need = (size_t)chunks * npix * 4 * sizeof(double);
+    if (need > s->partial_bytes) {
+        if (s->partial) {
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipFree(s->partial));
+            s->partial = nullptr;
+            s->partial_bytes = 0;
+        }
+        HIP_TRY(hipMalloc((void**)&s->partial, need));
+        s->partial_bytes = need;
+    }
+    if (ev0) HIP_TRY(hipEventRecord(ev0, st));
+    HIP_TRY(launch_trace(s->dev, samples, sample_begin, sample_end, chunk_len, chunks, tile_stride, tile_offset,
+                         seeds_dev, s->partial, st));
+    if (ev1) {
+        HIP_TRY(hipEventRecord(ev1, st));
+        s->events.emplace_back(ev0, ev1);
+    }
+    HIP_TRY(launch_reduce(s->partial, sums_dev, npix, chunks, (int)W, (int)H, tile_stride, tile_offset, st));
+    return PTMI_OK;
+}
+
+int ptmi_scene_set_timing(ptmi_scene* s, int enable) {
+    if (!s) return PTMI_ERR_ARG;
+    s->timing = enable != 0;
+    return PTMI_OK;
+}
+
+int ptmi_scene_kernel_time(ptmi_scene* s, double* total_ms, uint32_t* launches, char* err, size_t err_len) {
+    if (!s) {
+        set_err(err, err_len, "scene == NULL");
+        return PTMI_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    double tot = 0.0;
+    for (auto& e : s->events) {
+        HIP_TRY(hipEventSynchronize(e.second));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, e.first, e.second));
+        tot += ms;
+        s->spare.push_back(e.first);
+        s->spare.push_back(e.second);
+    }
+    if (total_ms) *total_ms = tot;
+    if (launches) *launches = (uint32_t)s->events.size();
+    s->events.clear();
+    return PTMI_OK;
+}
+
+int ptmi_finalize(const double* sums_dev, double* out_dev, uint32_t n_pixels, uint32_t samples, void* hip_stream,
+                  char* err, size_t err_len) {
+    if (!sums_dev || !out_dev || samples == 0) {
+        set_err(err, err_len, "bad finalize arguments");
+        return PTMI_ERR_ARG;
+    }
+    HIP_TRY(launch_finalize(sums_dev, out_dev, n_pixels, samples, (hipStream_t)hip_stream));
+    return PTMI_OK;
+}
+
+int ptmi_fill_seeds(double* seeds_dev, uint32_t n, uint64_t seed_stream, void* hip_stream, char* err,
+                    size_t err_len) {
+    if (!seeds_dev) {
+        set_err(err, err_len, "seeds_dev == NULL");
+        return PTMI_ERR_ARG;
+    }
+    HIP_TRY(launch_seeds(seeds_dev, n, seed_stream, (hipStream_t)hip_stream));
+    return PTMI_OK;
+}
+
+int ptmi_trace(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri, const void* groups,
+               uint32_t n_grp, int device_index, uint32_t samples, const void* camera, const double* seeds,
+               uint64_t seed_stream, const ptmi_textures* textures, double* out_rgba, char* err, size_t err_len) {
+    if (textures) {
+        for (int k = 0; k < 3; k++)
+            if (textures->count[k]) {
+                set_err(err, err_len, "texture arrays are not supported by this build");
+                return PTMI_ERR_UNSUPPORTED;
+            }
+    }
+    if (!out_rgba || samples == 0) {
+        set_err(err, err_len, "out_rgba == NULL or samples == 0");
+        return PTMI_ERR_ARG;
+    }
+    ptmi_scene* s = nullptr;
+    int rc = ptmi_scene_create(device_index, objects, n_obj, triangles, n_tri, groups, n_grp, camera, &s, err,
+                               err_len);
+    if (rc) return rc;
+    const uint32_t npix = s->width * s->height;
+    double *d_seeds = nullptr, *d_sums = nullptr;
+    hipStream_t st = nullptr;
+    auto fail = [&](int code) {
+        if (st) hipStreamDestroy(st);
+        if (d_seeds) hipFree(d_seeds);
+        if (d_sums) hipFree(d_sums);
+        ptmi_scene_destroy(s);
+        return code;
+    };
+#define TRY_OR_FAIL(call)                                                                         \
+    do {                                                                                          \
+        hipError_t e_ = (call);                                                                   \
+        if (e_ != hipSuccess) {                                                                   \
+            set_err(err, err_len, "%s failed: %s", #call, hipGetErrorString(e_));                 \
+            return fail(PTMI_ERR_HIP);                                                            \
+        }                                                                                         \
+    } while (0)
+    TRY_OR_FAIL(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    TRY_OR_FAIL(hipMalloc((void**)&d_seeds, (size_t)npix * sizeof(double)));
+    TRY_OR_FAIL(hipMalloc((void**)&d_sums, (size_t)npix * 4 * sizeof(double)));
+    if (seeds) {
+        TRY_OR_FAIL(hipMemcpyAsync(d_seeds, seeds, (size_t)npix * sizeof(double), hipMemcpyHostToDevice, st));
+    } else if ((rc = ptmi_fill_seeds(d_seeds, npix, seed_stream, st, err, err_len))) {
+        return fail(rc);
+    }
+    if ((rc = ptmi_scene_render(s, samples, 0, samples, 1, 0, d_seeds, d_sums, 0, st, err, err_len))) return fail(rc);
+    if ((rc = ptmi_finalize(d_sums, d_sums, npix, samples, st, err, err_len))) return fail(rc);
+    TRY_OR_FAIL(hipMemcpyAsync(out_rgba, d_sums, (size_t)npix * 4 * sizeof(double), hipMemcpyDeviceToHost, st));
+    TRY_OR_FAIL(hipStreamSynchronize(st));
+#undef TRY_OR_FAIL
+    fail(PTMI_OK);
+    return PTMI_OK;
+}
+
+}  // extern "C"

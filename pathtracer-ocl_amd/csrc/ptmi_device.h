@@ -1,0 +1,75 @@
+// ptmi_device.h -- HBM layout of a resident scene (host converter + gfx950 kernels).
+//
+// The reference's 1024/512/256-B packed records (tracer.cl:24-93) carry ~60 %
+// padding and force every work-item to copy whole objects around
+// (tracer.cl:846-849, 890).  Here they are split by access pattern:
+//   * DevObject  -- per-object data, read with wave-UNIFORM indices inside the
+//                   object loop (scalar s_load path, SGPR matrix operands);
+//   * DevNode    -- 64-B BVH node (box + triangle range + 2 children), preorder
+//                   numbering kept so traversal order == reference order;
+//   * DevTri     -- 96-B hot triangle data (p1, e1, e2) streamed by the
+//                   Moller-Trumbore loop; DevTriShade (n1..n3, color) is read
+//                   only for the winning triangle of a ray.
+// All doubles keep their 4th (w) component where the reference's double4 math
+// reads it, so results are bit-faithful (see DESIGN.md "Parity contract").
+#pragma once
+#include <stdint.h>
+
+namespace ptmi {
+
+struct alignas(16) DevObject {
+    double inv[16];    // object inverse (tracer.cl:547-548)
+    double inv_t[16];  // inverse transpose (tracer.cl:953)
+    double color[4];
+    double emission[4];
+    double refractive_index;
+    double min_y, max_y;  // cylinder clip (tracer.cl:426-434)
+    double reflectivity;
+    double bb_min[4], bb_max[4];  // group bounds in group space (tracer.cl:609)
+    int32_t type;                 // 0 plane 1 sphere 2 cylinder 3 cube 4 group, else ignored
+    int32_t child_count;          // group roots (tracer.cl:617-621)
+    int32_t child_base;           // index of the first root in DevScene::roots
+    int32_t pad;
+};
+
+struct alignas(16) DevNode {
+    double bb_min[3];
+    double bb_max[3];
+    int32_t tri_offset, tri_count;
+    int32_t child0, child1;  // > 0 means present (tracer.cl:683, 704)
+};
+static_assert(sizeof(DevNode) == 64, "DevNode must stay 64 B");
+
+struct alignas(16) DevTri {
+    double p1[4];
+    double e1[4];
+    double e2[4];
+};
+static_assert(sizeof(DevTri) == 96, "DevTri must stay 96 B");
+
+struct alignas(16) DevTriShade {
+    double n1[4], n2[4], n3[4];
+    double color[4];
+};
+
+struct DevCamera {
+    int32_t width, height;
+    double pixel_size, half_width, half_height, aperture, focal_length;
+    double inv[16];
+};
+
+// Passed BY VALUE as a kernel argument: everything here is wave-uniform.
+struct DevScene {
+    const DevObject* objs;
+    const int32_t* roots;  // concatenated group roots of all type-4 objects
+    const DevNode* nodes;
+    const DevTri* tris;
+    const DevTriShade* tri_shade;
+    uint32_t n_obj, n_nodes, n_tri, pad;
+    DevCamera cam;
+};
+
+constexpr int kTile = 8;          // a wave64 covers an 8x8 pixel tile
+constexpr int kWavesPerBlock = 4; // 256-thread workgroups
+
+}  // namespace ptmi

@@ -1,0 +1,197 @@
+"""ctypes binding of libptmi.so (include/ptmi.h).
+
+``Trace`` mirrors the reference's Go entry point
+``internal/ocl.Trace(objects, triangles, groups, deviceIndex, samples, camera,
+textures, sphereTextures, cubeTextures) []float64`` (ocltracer.go:98-226): same
+argument meaning, same record bytes, same float64 RGBA result.  Where the Go code
+calls ``logrus.Fatalf`` this raises ``PtmiError`` (the library returned an error
+code; nothing falls back to another implementation).
+
+``Scene`` exposes the resident-scene API (scene uploaded to HBM once, frames
+rendered from device buffers on a caller's HIP stream) used by bench.py and
+the multi-GPU driver; device buffers are passed as raw pointers (e.g.
+``tensor.data_ptr()``), so the C ABI stays free of torch types.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _runtime, layout
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PTMI_LIB", os.path.join(_HERE, "..", "build", "libptmi.so"))
+
+PTMI_OK, PTMI_ERR_ARG, PTMI_ERR_DEVICE, PTMI_ERR_HIP, PTMI_ERR_UNSUPPORTED, PTMI_ERR_NOMEM = 0, -1, -2, -3, -4, -5
+
+EXPORTS = ("ptmi_trace", "ptmi_device_count", "ptmi_device_name", "ptmi_scene_create", "ptmi_scene_destroy",
+           "ptmi_scene_size", "ptmi_scene_render", "ptmi_finalize", "ptmi_fill_seeds", "ptmi_build_info",
+           "ptmi_scene_set_timing", "ptmi_scene_kernel_time")
+
+
+class PtmiError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("libptmi error %d: %s" % (code, msg))
+        self.code = code
+
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load libptmi.so (raises if it is missing: there is no fallback path)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = os.path.abspath(path or LIB_PATH)
+    _runtime.preload()
+    if not os.path.exists(p):
+        raise FileNotFoundError("libptmi.so not built (%s): run `make -C pathtracer-ocl_amd`" % p)
+    lib = ctypes.CDLL(p)
+    vp, u32, i32, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_size_t
+    cp = ctypes.c_char_p
+    lib.ptmi_trace.restype = i32
+    lib.ptmi_trace.argtypes = [vp, u32, vp, u32, vp, u32, i32, u32, vp, vp, ctypes.c_uint64, vp, vp, cp, sz]
+    lib.ptmi_device_count.restype = i32
+    lib.ptmi_device_count.argtypes = []
+    lib.ptmi_device_name.restype = i32
+    lib.ptmi_device_name.argtypes = [i32, cp, sz]
+    lib.ptmi_scene_create.restype = i32
+    lib.ptmi_scene_create.argtypes = [i32, vp, u32, vp, u32, vp, u32, vp, ctypes.POINTER(vp), cp, sz]
+    lib.ptmi_scene_destroy.restype = None
+    lib.ptmi_scene_destroy.argtypes = [vp]
+    lib.ptmi_scene_size.restype = i32
+    lib.ptmi_scene_size.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32)]
+    lib.ptmi_scene_render.restype = i32
+    lib.ptmi_scene_render.argtypes = [vp, u32, u32, u32, u32, u32, vp, vp, u32, vp, cp, sz]
+    lib.ptmi_finalize.restype = i32
+    lib.ptmi_finalize.argtypes = [vp, vp, u32, u32, vp, cp, sz]
+    lib.ptmi_fill_seeds.restype = i32
+    lib.ptmi_fill_seeds.argtypes = [vp, u32, ctypes.c_uint64, vp, cp, sz]
+    lib.ptmi_scene_set_timing.restype = i32
+    lib.ptmi_scene_set_timing.argtypes = [vp, i32]
+    lib.ptmi_scene_kernel_time.restype = i32
+    lib.ptmi_scene_kernel_time.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u32), cp, sz]
+    lib.ptmi_build_info.restype = cp
+    lib.ptmi_build_info.argtypes = []
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(rc, err):
+    if rc != PTMI_OK:
+        raise PtmiError(rc, err.value.decode(errors="replace"))
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None and len(a) else None
+
+
+def _records(objects, triangles, groups, camera):
+    objects = np.ascontiguousarray(objects)
+    triangles = np.ascontiguousarray(triangles) if triangles is not None else np.zeros(0, layout.TRIANGLE_DTYPE)
+    groups = np.ascontiguousarray(groups) if groups is not None else np.zeros(0, layout.GROUP_DTYPE)
+    camera = np.ascontiguousarray(np.asarray(camera).reshape(1))
+    for arr, dt, name in ((objects, layout.OBJECT_DTYPE, "objects"), (triangles, layout.TRIANGLE_DTYPE, "triangles"),
+                          (groups, layout.GROUP_DTYPE, "groups"), (camera, layout.CAMERA_DTYPE, "camera")):
+        if arr.dtype.itemsize != dt.itemsize:
+            raise TypeError("%s: expected %d-byte records, got %d" % (name, dt.itemsize, arr.dtype.itemsize))
+    return objects, triangles, groups, camera
+
+
+def device_count():
+    return load_library().ptmi_device_count()
+
+
+def device_name(i):
+    buf = ctypes.create_string_buffer(256)
+    rc = load_library().ptmi_device_name(i, buf, len(buf))
+    if rc:
+        raise PtmiError(rc, "no device %d" % i)
+    return buf.value.decode()
+
+
+def Trace(objects, triangles, groups, deviceIndex, samples, camera, textures=None, sphereTextures=None,
+          cubeTextures=None, seeds=None, seed_stream=0):
+    """Drop-in for ocl.Trace (ocltracer.go:98-100).  Returns float64 RGBA, len W*H*4.
+
+    ``seeds``: W*H per-pixel seeds (the Go side's rand.Float64() per pixel); None
+    lets the library generate them from ``seed_stream``.
+    """
+    if textures or sphereTextures or cubeTextures:
+        raise PtmiError(PTMI_ERR_UNSUPPORTED, "texture arrays are not supported by this build")
+    lib = load_library()
+    objects, triangles, groups, camera = _records(objects, triangles, groups, camera)
+    w, h = int(camera["width"][0]), int(camera["height"][0])
+    if seeds is not None:
+        seeds = np.ascontiguousarray(seeds, dtype=np.float64)
+        if seeds.size != w * h:
+            raise ValueError("seeds: expected %d values, got %d" % (w * h, seeds.size))
+    out = np.empty(w * h * 4, dtype=np.float64)
+    err = ctypes.create_string_buffer(1024)
+    rc = lib.ptmi_trace(_ptr(objects), len(objects), _ptr(triangles), len(triangles), _ptr(groups), len(groups),
+                        int(deviceIndex), int(samples), _ptr(camera), _ptr(seeds), int(seed_stream), None,
+                        out.ctypes.data_as(ctypes.c_void_p), err, len(err))
+    _check(rc, err)
+    return out
+
+
+class Scene:
+    """A scene resident on one device (ptmi_scene_*)."""
+
+    def __init__(self, device_index, objects, triangles, groups, camera):
+        self._lib = load_library()
+        objects, triangles, groups, camera = _records(objects, triangles, groups, camera)
+        handle = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(1024)
+        rc = self._lib.ptmi_scene_create(int(device_index), _ptr(objects), len(objects), _ptr(triangles),
+                                         len(triangles), _ptr(groups), len(groups), _ptr(camera),
+                                         ctypes.byref(handle), err, len(err))
+        _check(rc, err)
+        self._h = handle
+        w, h = ctypes.c_uint32(), ctypes.c_uint32()
+        self._lib.ptmi_scene_size(self._h, ctypes.byref(w), ctypes.byref(h))
+        self.width, self.height = w.value, h.value
+
+    def render(self, samples, sample_begin, sample_end, seeds_ptr, sums_ptr, tile_stride=1, tile_offset=0,
+               chunks=0, stream=0):
+        err = ctypes.create_string_buffer(1024)
+        rc = self._lib.ptmi_scene_render(self._h, samples, sample_begin, sample_end, tile_stride, tile_offset,
+                                         ctypes.c_void_p(seeds_ptr), ctypes.c_void_p(sums_ptr), chunks,
+                                         ctypes.c_void_p(stream), err, len(err))
+        _check(rc, err)
+
+    def finalize(self, sums_ptr, out_ptr, samples, stream=0):
+        err = ctypes.create_string_buffer(1024)
+        rc = self._lib.ptmi_finalize(ctypes.c_void_p(sums_ptr), ctypes.c_void_p(out_ptr),
+                                     self.width * self.height, samples, ctypes.c_void_p(stream), err, len(err))
+        _check(rc, err)
+
+    def set_timing(self, enable=True):
+        self._lib.ptmi_scene_set_timing(self._h, 1 if enable else 0)
+
+    def kernel_time(self):
+        """(summed trace_kernel ms, launches) since the last call (waits for them)."""
+        ms, n = ctypes.c_double(), ctypes.c_uint32()
+        err = ctypes.create_string_buffer(512)
+        _check(self._lib.ptmi_scene_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n), err, len(err)), err)
+        return ms.value, n.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.ptmi_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def fill_seeds(seeds_ptr, n, seed_stream, stream=0):
+    lib = load_library()
+    err = ctypes.create_string_buffer(256)
+    _check(lib.ptmi_fill_seeds(ctypes.c_void_p(seeds_ptr), n, seed_stream, ctypes.c_void_p(stream), err, len(err)),
+           err)

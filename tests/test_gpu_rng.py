@@ -1,0 +1,42 @@
+"""The reference RNG's float sin (tracer.cl:314-317 -> ocml __ocml_sin_f32):
+exhaustive bit-identity of the oracle's restatement (oracle/ocml_sinf.h) with
+the GPU device library over all 2^32 float inputs, and replay of ocml values
+on the host CPU (same code the CPU oracle runs)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+
+pytestmark = pytest.mark.gpu
+LIB = os.path.join(os.path.dirname(__file__), "gpu_probe", "build", "libsinfprobe.so")
+
+
+def _lib():
+    if not os.path.exists(LIB):
+        pytest.fail("probe library not built: %s (run __graft_entry__.build())" % LIB)
+    import torch  # noqa: F401  one HIP runtime per process (ptmi/_runtime.py)
+    lib = ctypes.CDLL(LIB)
+    lib.probe_sinf_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
+    lib.probe_sinf_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+    return lib
+
+
+def test_restated_sinf_bit_identical_all_floats():
+    lib = _lib()
+    m, f = ctypes.c_ulonglong(), ctypes.c_uint()
+    assert lib.probe_sinf_all(ctypes.byref(m), ctypes.byref(f)) == 0
+    assert m.value == 0, "%d mismatches, first input bits 0x%08x" % (m.value, f.value)
+
+
+def test_cpu_restatement_replays_gpu_ocml():
+    lib = _lib()
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(-1e9, 1e9, 50000), rng.uniform(-200, 200, 50000),
+                        rng.uniform(0, 8e8, 50000)]).astype(np.float32)
+    gpu = np.empty_like(x)
+    assert lib.probe_sinf_eval(x.ctypes.data, gpu.ctypes.data, x.size) == 0
+    cpu = np.array([pyoracle.sinf(float(v)) for v in x[:20000]], dtype=np.float32)
+    assert np.array_equal(cpu.view(np.uint32), gpu[:20000].view(np.uint32))
