@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -16,14 +17,15 @@
 #include "ptmi_device.h"
 
 namespace ptmi {
-hipError_t launch_trace(const DevScene& S, uint32_t samples, uint32_t s_begin, uint32_t s_end, uint32_t chunk_len,
-                        uint32_t nchunks, uint32_t tile_stride, uint32_t tile_offset, const double* seeds,
-                        double* out, hipStream_t st);
+hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, uint32_t s_begin, uint32_t s_end,
+                        uint32_t chunk_len, uint32_t nchunks, uint32_t tile_stride, uint32_t tile_offset,
+                        const double* seeds, double* out, hipStream_t st);
 hipError_t launch_reduce(const double* part, double* sums, uint32_t npix, uint32_t nchunks, int W, int H,
                          uint32_t tile_stride, uint32_t tile_offset, hipStream_t st);
 hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint32_t samples, hipStream_t st);
 hipError_t launch_seeds(double* seeds, uint32_t n, uint64_t stream, hipStream_t st);
-const void* trace_kernel_symbol();
+hipError_t launch_plane_normals(DevObject* objs, int n, hipStream_t st);
+const void* trace_kernel_symbol(int flags);
 }  // namespace ptmi
 
 using namespace ptmi;
@@ -31,11 +33,12 @@ using namespace ptmi;
 struct ptmi_scene {
     int device = 0;
     DevScene dev{};
-    void* buffers[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    void* buffers[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     double* partial = nullptr;  // chunk partial sums, grown on demand
     size_t partial_bytes = 0;
     int resident_waves = 0;  // device-wide resident waves of trace_kernel
     uint32_t width = 0, height = 0;
+    int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pending (start, stop) pairs
     std::vector<hipEvent_t> spare;
@@ -91,10 +94,24 @@ int check_device(int idx, char* err, size_t err_len) {
 }
 
 // Convert + validate the packed reference records (layout.py / tracer.cl:24-93).
+// Zero-pattern predicates (exact zeros, +-0 included).
+bool is_st_pattern(const double* m) {  // [a 0 0 d; 0 b 0 e; 0 0 c f; 0 0 0 g]
+    static const int z[] = {1, 2, 4, 6, 8, 9, 12, 13, 14};
+    for (int i : z)
+        if (m[i] != 0.0) return false;
+    return true;
+}
+bool is_diag3(const double* m) {  // rows 0-2 diagonal (row 3 unused)
+    static const int z[] = {1, 2, 3, 4, 6, 7, 8, 9, 11};
+    for (int i : z)
+        if (m[i] != 0.0) return false;
+    return true;
+}
+
 int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, uint32_t n_tri, const uint8_t* groups,
                   uint32_t n_grp, const uint8_t* camera, std::vector<DevObject>& objs, std::vector<int32_t>& roots,
                   std::vector<DevNode>& nodes, std::vector<DevTri>& ht, std::vector<DevTriShade>& st, DevCamera& cam,
-                  char* err, size_t err_len) {
+                  int32_t run_end[5], char* err, size_t err_len) {
     if (!objects || n_obj == 0 || n_obj > PTMI_MAX_OBJECTS) {
         set_err(err, err_len, "need 1..%d objects (tracer.cl:846 __local object objects[16]), got %u",
                 PTMI_MAX_OBJECTS, n_obj);
@@ -116,11 +133,12 @@ int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, u
         set_err(err, err_len, "bad camera size %dx%d", cam.width, cam.height);
         return PTMI_ERR_ARG;
     }
-    objs.resize(n_obj);
+    std::vector<DevObject> all(n_obj);
     for (uint32_t i = 0; i < n_obj; i++) {
         const uint8_t* b = objects + (size_t)PTMI_OBJECT_BYTES * i;
-        DevObject& o = objs[i];
+        DevObject& o = all[i];
         std::memset(&o, 0, sizeof o);
+        o.key = (int32_t)i;
         std::memcpy(o.inv, b + 128, 128);
         std::memcpy(o.inv_t, b + 256, 128);
         std::memcpy(o.color, b + 384, 32);
@@ -132,6 +150,8 @@ int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, u
         o.max_y = rd<double>(b + 472);
         o.reflectivity = rd<double>(b + 480);
         std::memcpy(o.bb_min, b + 520, 32);
+        o.st = is_st_pattern(o.inv) ? 1 : 0;
+        o.invt_diag = is_diag3(o.inv_t) ? 1 : 0;
         std::memcpy(o.bb_max, b + 552, 32);
         if (b[844] || b[846]) {
             set_err(err, err_len,
@@ -158,6 +178,15 @@ int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, u
             }
             o.child_count = cc;
         }
+    }
+    // Intersectable objects in type runs [planes | spheres | cylinders | cubes |
+    // groups], list order inside a run.  Types > 4 and groups without BVH roots
+    // can never record an intersection (tracer.cl:551-720) and are left out.
+    objs.clear();
+    for (int t = 0; t < 5; t++) {
+        for (const DevObject& o : all)
+            if (o.type == t && (t != 4 || o.child_count > 0)) objs.push_back(o);
+        run_end[t] = (int32_t)objs.size();
     }
     nodes.resize(n_grp);
     for (uint32_t g = 0; g < n_grp; g++) {
@@ -217,7 +246,7 @@ int ptmi_device_name(int device_index, char* buf, size_t len) {
 }
 
 const char* ptmi_build_info(void) {
-    return "ptmi abi=1 arch=gfx950 fp=fp64 contract=off kernels=trace_kernel,reduce_chunks_kernel,finalize_kernel";
+    return "ptmi abi=1 arch=gfx950 fp=fp64 contract=off kernels=trace_kernel<F>,reduce_chunks_kernel,finalize_kernel";
 }
 
 int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
@@ -237,11 +266,21 @@ int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, con
     std::vector<DevTri> ht;
     std::vector<DevTriShade> st;
     DevCamera cam{};
+    int32_t run_end[5];
     rc = convert_scene((const uint8_t*)objects, n_obj, (const uint8_t*)triangles, n_tri, (const uint8_t*)groups, n_grp,
-                       (const uint8_t*)camera, objs, roots, nodes, ht, st, cam, err, err_len);
+                       (const uint8_t*)camera, objs, roots, nodes, ht, st, cam, run_end, err, err_len);
     if (rc) return rc;
+    int flags = 0;
+    for (const DevObject& o : objs) {
+        if (o.type == 4) flags |= 1;                                    // F_GROUPS
+        if (o.type == 2 || o.type == 3) flags |= 2;                     // F_CYLCUBE
+        if (o.reflectivity != 0.0 || o.refractive_index != 1.0) flags |= 4;  // F_MATERIALS
+    }
+    if (cam.aperture != 0) flags |= 8;                                  // F_DOF
+    if (const char* f = getenv("PTMI_FORCE_FLAGS")) flags = atoi(f) & 15;  // testing: force the generic path
     HIP_TRY(hipSetDevice(device_index));
     ptmi_scene* s = new ptmi_scene();
+    s->flags = flags;
     s->device = device_index;
     s->width = (uint32_t)cam.width;
     s->height = (uint32_t)cam.height;
@@ -252,11 +291,51 @@ int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, con
         return rc;
     }
     s->dev.objs = (const DevObject*)s->buffers[0];
+    for (int t = 0; t < 5; t++) s->dev.run_end[t] = run_end[t];
+    {  // compact plane / scale+translate sphere records (ptmi_device.h)
+        std::vector<PlaneRec> pl;
+        std::vector<SphereRec> sp;
+        for (size_t k = 0; k < objs.size(); k++) {
+            const DevObject& o = objs[k];
+            if (o.type == 0) {
+                PlaneRec r{};
+                std::memcpy(r.row1, o.inv + 4, 32);
+                r.slot = (int32_t)k;
+                r.key = o.key;
+                pl.push_back(r);
+            } else if (o.type == 1 && o.st) {
+                SphereRec r{};
+                r.m0 = o.inv[0];
+                r.m3 = o.inv[3];
+                r.m5 = o.inv[5];
+                r.m7 = o.inv[7];
+                r.m10 = o.inv[10];
+                r.m11 = o.inv[11];
+                r.m15 = o.inv[15];
+                r.slot = (int32_t)k;
+                r.key = o.key;
+                sp.push_back(r);
+            }
+        }
+        if ((rc = upload(pl, &s->buffers[5], err, err_len)) || (rc = upload(sp, &s->buffers[6], err, err_len))) {
+            ptmi_scene_destroy(s);
+            return rc;
+        }
+        s->dev.planes = (const PlaneRec*)s->buffers[5];
+        s->dev.n_planes = (int32_t)pl.size();
+        s->dev.spheres = (const SphereRec*)s->buffers[6];
+        s->dev.n_spheres_st = (int32_t)sp.size();
+    }
+    if (!objs.empty()) {
+        HIP_TRY(launch_plane_normals((DevObject*)s->buffers[0], (int)objs.size(), nullptr));
+        HIP_TRY(hipDeviceSynchronize());
+    }
     s->dev.roots = (const int32_t*)s->buffers[1];
     s->dev.nodes = (const DevNode*)s->buffers[2];
     s->dev.tris = (const DevTri*)s->buffers[3];
     s->dev.tri_shade = (const DevTriShade*)s->buffers[4];
-    s->dev.n_obj = n_obj;
+    s->dev.n_obj = (uint32_t)objs.size();
+    s->dev.n_list = n_obj;
     s->dev.n_nodes = n_grp;
     s->dev.n_tri = n_tri;
     s->dev.cam = cam;
@@ -264,7 +343,7 @@ int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, con
     HIP_TRY(hipGetDeviceProperties(&p, device_index));
     s->resident_waves = p.multiProcessorCount * 16;  // refined below from the occupancy query
     int blocks_per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, trace_kernel_symbol(), 256, 0) ==
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, trace_kernel_symbol(s->flags), 256, 0) ==
             hipSuccess &&
         blocks_per_cu > 0)
         s->resident_waves = p.multiProcessorCount * blocks_per_cu * kWavesPerBlock;
@@ -331,7 +410,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     if (chunks == 1) {
         if (tile_stride > 1) HIP_TRY(hipMemsetAsync(sums_dev, 0, (size_t)npix * 4 * sizeof(double), st));
         if (ev0) HIP_TRY(hipEventRecord(ev0, st));
-        HIP_TRY(launch_trace(s->dev, samples, sample_begin, sample_end, chunk_len, 1, tile_stride, tile_offset,
+        HIP_TRY(launch_trace(s->dev, s->flags, samples, sample_begin, sample_end, chunk_len, 1, tile_stride, tile_offset,
                              seeds_dev, sums_dev, st));
         if (ev1) {
             HIP_TRY(hipEventRecord(ev1, st));
@@ -351,7 +430,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         s->partial_bytes = need;
     }
     if (ev0) HIP_TRY(hipEventRecord(ev0, st));
-    HIP_TRY(launch_trace(s->dev, samples, sample_begin, sample_end, chunk_len, chunks, tile_stride, tile_offset,
+    HIP_TRY(launch_trace(s->dev, s->flags, samples, sample_begin, sample_end, chunk_len, chunks, tile_stride, tile_offset,
                          seeds_dev, s->partial, st));
     if (ev1) {
         HIP_TRY(hipEventRecord(ev1, st));

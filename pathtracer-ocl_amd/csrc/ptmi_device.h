@@ -26,10 +26,15 @@ struct alignas(16) DevObject {
     double min_y, max_y;  // cylinder clip (tracer.cl:426-434)
     double reflectivity;
     double bb_min[4], bb_max[4];  // group bounds in group space (tracer.cl:609)
-    int32_t type;                 // 0 plane 1 sphere 2 cylinder 3 cube 4 group, else ignored
+    double plane_n[4];            // planes: normalize(mul(invT, (0,1,0,0))) with w = 0 (tracer.cl:913, 953-955),
+                                  // computed on the device at upload with the kernel's own arithmetic
+    int32_t type;                 // 0 plane 1 sphere 2 cylinder 3 cube 4 group
     int32_t child_count;          // group roots (tracer.cl:617-621)
     int32_t child_base;           // index of the first root in DevScene::roots
-    int32_t pad;
+    int32_t key;                  // index in the reference's object list (tie-break order)
+    int32_t st;                   // inv has the scale+translate zero pattern (see xform_st)
+    int32_t invt_diag;            // rows 0-2 of inv_t are diagonal
+    int32_t pad[2];
 };
 
 struct alignas(16) DevNode {
@@ -58,14 +63,37 @@ struct DevCamera {
     double inv[16];
 };
 
+// Compact records for the two hottest intersection loops (read with scalar
+// loads; one object = one or two s_load_dwordx8/x16):
+struct alignas(16) PlaneRec {  // intersectPlane needs row 1 of the inverse only
+    double row1[4];
+    int32_t slot, key;  // DevScene::objs slot, reference list index
+    int32_t pad[2];
+};
+struct alignas(16) SphereRec {  // sphere with the scale+translate inverse pattern
+    double m0, m3, m5, m7, m10, m11, m15, pad;
+    int32_t slot, key;
+    int32_t pad2[2];
+};
+
 // Passed BY VALUE as a kernel argument: everything here is wave-uniform.
+// objs[] holds the intersectable objects sorted into type runs
+// [planes | spheres | cylinders | cubes | groups]; run_end[t] is the end of run t.
 struct DevScene {
     const DevObject* objs;
+    int32_t run_end[5];  // slots [run_end[t-1], run_end[t]) hold type t
+    int32_t n_planes;
+    const PlaneRec* planes;      // all planes
+    const SphereRec* spheres;    // scale+translate spheres (the rest: DevObject path)
+    int32_t n_spheres_st;
+    int32_t pad1;
     const int32_t* roots;  // concatenated group roots of all type-4 objects
     const DevNode* nodes;
     const DevTri* tris;
     const DevTriShade* tri_shade;
-    uint32_t n_obj, n_nodes, n_tri, pad;
+    uint32_t n_obj;   // intersectable objects in objs[]
+    uint32_t n_nodes, n_tri;
+    uint32_t n_list;  // numObjects of the reference's list (fgi = seed / numObjects, tracer.cl:840)
     DevCamera cam;
 };
 

@@ -72,6 +72,23 @@ __device__ __forceinline__ d4 mat_mul(const double* __restrict__ m, d4 v) {
               ((m[12] * v.x + m[13] * v.y) + m[14] * v.z) + m[15] * v.w);
 }
 
+// mul() for a matrix with the scale+translate zero pattern
+//   [a 0 0 d; 0 b 0 e; 0 0 c f; 0 0 0 g]   (DevObject::st, checked on the host).
+// The reference's ((m0 x + m1 y) + m2 z) + m3 w with m1 = m2 = +-0 equals
+// m0 x + m3 w bit-for-bit for a finite ray, up to the sign of an exact-zero
+// result, which no branch or output of the path depends on (rays are finite
+// here: see PathState::dead).
+__device__ __forceinline__ d4 xform_st(const double* __restrict__ m, d4 v) {
+    return mk(m[0] * v.x + m[3] * v.w, m[5] * v.y + m[7] * v.w, m[10] * v.z + m[11] * v.w, m[15] * v.w);
+}
+__device__ __forceinline__ d4 xform(const double* __restrict__ m, bool st, d4 v) {
+    return st ? xform_st(m, v) : mat_mul(m, v);
+}
+// Row 1 of mul() only (intersectPlane reads nothing else, tracer.cl:478-483).
+__device__ __forceinline__ double row1(const double* __restrict__ m, bool st, d4 v) {
+    return st ? m[5] * v.y + m[7] * v.w : ((m[4] * v.x + m[5] * v.y) + m[6] * v.z) + m[7] * v.w;
+}
+
 // noise3D (tracer.cl:314-317): float math, ocml sin_f32, ocml fract_f32.
 __device__ __forceinline__ float noise3d(float x, float y, float z) {
     float a = x * 112.9898f;
@@ -109,25 +126,33 @@ __device__ __forceinline__ bool ray_box(d4 o, d4 d, const double* mn, const doub
 
 struct Hit {
     double t;
-    int obj;
+    int obj;  // slot in DevScene::objs (type-run order)
+    int key;  // the object's index in the reference's list
     int tri;
     double u, v;
 };
 
-// The reference records every candidate then picks the first t > EPSILON that
-// is strictly below the running best (start 1024) in recording order
-// (tracer.cl:728-739); reducing on the fly in the same order is identical.
-__device__ __forceinline__ void consider(Hit& h, double t, int obj) {
-    if (t > kEps && t < h.t) {
+// The reference records every candidate, then picks the FIRST (in recording
+// order) t > EPSILON that is strictly below the running best, which starts at
+// 1024 (tracer.cl:728-739).  Objects are visited here in type runs, not in
+// list order, so a tie in t is broken by the object's list index: the winner is
+// the lexicographic minimum (t, key) -- the same candidate.  Candidates of one
+// object are still produced in the reference's order (strict < keeps the first).
+__device__ __forceinline__ bool better(const Hit& h, double t, int key) {
+    return t > kEps && (t < h.t || (t == h.t && key < h.key));
+}
+__device__ __forceinline__ void consider(Hit& h, double t, int obj, int key) {
+    if (better(h, t, key)) {
         h.t = t;
         h.obj = obj;
+        h.key = key;
         h.tri = -1;
     }
 }
 
 // Stack-based BVH walk of one group root, in the reference's preorder
 // (tracer.cl:621-719), Moller-Trumbore per triangle (640-675).
-__device__ __noinline__ void walk_group(const DevScene& S, int root, int obj, d4 o, d4 d, Hit& h) {
+__device__ __noinline__ void walk_group(const DevScene& S, int root, int obj, int key, d4 o, d4 d, Hit& h) {
     int stack[64];
     int sidx = 0;
     int cur_idx = root;
@@ -149,9 +174,10 @@ __device__ __noinline__ void walk_group(const DevScene& S, int root, int obj, d4
                 double v = f * dot4(d, oce1);
                 if (v < 0 || (u + v) > 1) continue;
                 double t = f * dot4(e2, oce1);
-                if (t > kEps && t < h.t) {
+                if (better(h, t, key)) {
                     h.t = t;
                     h.obj = obj;
+                    h.key = key;
                     h.tri = n;
                     h.u = u;
                     h.v = v;
@@ -177,32 +203,75 @@ __device__ __noinline__ void walk_group(const DevScene& S, int root, int obj, d4
     }
 }
 
-// findClosestIntersection (tracer.cl:537-742).  The object loop index is
-// wave-uniform, so the per-object matrices come in through scalar loads.
+// Scene-feature flags: the host inspects the records once and launches the
+// instantiation that compiles out absent object types / materials / DoF.  Every
+// type or material present in the scene keeps its flag, so the result is the
+// same as the generic path.
+enum : int {
+    F_GROUPS = 1,     // a type-4 object with BVH roots
+    F_CYLCUBE = 2,    // cylinders or cubes present
+    F_MATERIALS = 4,  // reflectivity != 0 or refractive index != 1 somewhere
+    F_DOF = 8,        // camera aperture != 0
+    F_ALL = 15
+};
+
+// Candidate update as selects (no exec-mask branching).  t > EPSILON implies
+// the reference's `t != 0.0` recording test.
+__device__ __forceinline__ void consider_sel(Hit& h, double t, int obj, int key) {
+    const bool c = better(h, t, key);
+    h.t = c ? t : h.t;
+    h.obj = c ? obj : h.obj;
+    h.key = c ? key : h.key;
+    h.tri = c ? -1 : h.tri;
+}
+
+// intersectSphere (tracer.cl:448-476) on an object-space ray.
+__device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int key) {
+    d4 vtc = mk(o.x - 0.0, o.y - 0.0, o.z - 0.0, o.w - 1.0);
+    double a = dot4(d, d);
+    double b = 2.0 * dot4(d, vtc);
+    double c = dot4(vtc, vtc) - 1.0;
+    double disc = (b * b) - 4 * a * c;
+    if (disc > 0.0) {
+        double sq = sqrt(disc);
+        double t1 = (-b - sq) / (2 * a);
+        double t2 = (-b + sq) / (2 * a);
+        consider_sel(h, t1, slot, key);
+        consider_sel(h, t2, slot, key);
+    }
+}
+
+// findClosestIntersection (tracer.cl:537-742), one loop per object type.  Loop
+// indices are wave-uniform, so object data arrives through scalar loads.
+template <int FL>
 __device__ __forceinline__ Hit find_closest(const DevScene& S, d4 ro, d4 rd) {
-    Hit h{1024.0, -1, -1, 0.0, 0.0};
-    for (uint32_t j = 0; j < S.n_obj; j++) {
+    Hit h{1024.0, -1, -1, -1, 0.0, 0.0};
+    for (int p = 0; p < S.n_planes; p++) {  // intersectPlane (478-483): row 1 only
+        const PlaneRec& P = S.planes[p];
+        const double oy = ((P.row1[0] * ro.x + P.row1[1] * ro.y) + P.row1[2] * ro.z) + P.row1[3] * ro.w;
+        const double dy = ((P.row1[0] * rd.x + P.row1[1] * rd.y) + P.row1[2] * rd.z) + P.row1[3] * rd.w;
+        const double q = -oy / dy;
+        consider_sel(h, fabs(dy) > kEps ? q : 0.0, P.slot, P.key);
+    }
+    for (int q = 0; q < S.n_spheres_st; q++) {  // scale+translate spheres
+        const SphereRec& Q = S.spheres[q];
+        const d4 o = mk(Q.m0 * ro.x + Q.m3 * ro.w, Q.m5 * ro.y + Q.m7 * ro.w, Q.m10 * ro.z + Q.m11 * ro.w,
+                        Q.m15 * ro.w);
+        const d4 d = mk(Q.m0 * rd.x + Q.m3 * rd.w, Q.m5 * rd.y + Q.m7 * rd.w, Q.m10 * rd.z + Q.m11 * rd.w,
+                        Q.m15 * rd.w);
+        sphere_test(h, o, d, Q.slot, Q.key);
+    }
+    int j = S.run_end[0];
+    for (; j < S.run_end[1]; j++) {  // spheres with other matrices
         const DevObject& ob = S.objs[j];
-        const int type = ob.type;
-        d4 o = mat_mul(ob.inv, ro);
-        d4 d = mat_mul(ob.inv, rd);
-        if (type == 0) {  // intersectPlane (478-483)
-            double t = fabs(d.y) > kEps ? -o.y / d.y : 0.0;
-            if (t != 0.0) consider(h, t, (int)j);
-        } else if (type == 1) {  // intersectSphere (448-476)
-            d4 vtc = mk(o.x - 0.0, o.y - 0.0, o.z - 0.0, o.w - 1.0);
-            double a = dot4(d, d);
-            double b = 2.0 * dot4(d, vtc);
-            double c = dot4(vtc, vtc) - 1.0;
-            double disc = (b * b) - 4 * a * c;
-            if (disc > 0.0) {
-                double sq = sqrt(disc);
-                double t1 = (-b - sq) / (2 * a);
-                double t2 = (-b + sq) / (2 * a);
-                if (t1 != 0.0) consider(h, t1, (int)j);
-                if (t2 != 0.0) consider(h, t2, (int)j);
-            }
-        } else if (type == 2) {  // intersectCylinder (396-446), caps disabled
+        if (ob.st) continue;  // in S.spheres
+        sphere_test(h, mat_mul(ob.inv, ro), mat_mul(ob.inv, rd), j, ob.key);
+    }
+    if (FL & F_CYLCUBE) {
+        for (; j < S.run_end[2]; j++) {  // cylinders: intersectCylinder (396-446), caps disabled
+            const DevObject& ob = S.objs[j];
+            d4 o = xform(ob.inv, ob.st, ro);
+            d4 d = xform(ob.inv, ob.st, rd);
             double a = d.x * d.x + d.z * d.z;
             if (!(fabs(a) < kEps)) {
                 double b = 2 * o.x * d.x + 2 * o.z * d.z;
@@ -216,23 +285,34 @@ __device__ __forceinline__ Hit find_closest(const DevScene& S, d4 ro, d4 rd) {
                     double y1 = o.y + t1 * d.y;
                     double r0 = (y0 > ob.min_y && y0 < ob.max_y) ? t0 : 0.0;
                     double r1 = (y1 > ob.min_y && y1 < ob.max_y) ? t1 : 0.0;
-                    if (r0 != 0) consider(h, r0, (int)j);
-                    if (r1 != 0) consider(h, r1, (int)j);
+                    consider_sel(h, r0, j, ob.key);
+                    consider_sel(h, r1, j, ob.key);
                 }
             }
-        } else if (type == 3) {  // intersectCube (378-394)
+        }
+        for (; j < S.run_end[3]; j++) {  // cubes: intersectCube (378-394)
+            const DevObject& ob = S.objs[j];
+            d4 o = xform(ob.inv, ob.st, ro);
+            d4 d = xform(ob.inv, ob.st, rd);
             double x0, x1, y0, y1, z0, z1;
             check_axis(o.x, d.x, -1.0, 1.0, x0, x1);
             check_axis(o.y, d.y, -1.0, 1.0, y0, y1);
             check_axis(o.z, d.z, -1.0, 1.0, z0, z1);
             double tmin = max3(x0, y0, z0), tmax = min3(x1, y1, z1);
             if (!(tmin > tmax)) {
-                if (tmin != 0.0) consider(h, tmin, (int)j);
-                if (tmax != 0.0) consider(h, tmax, (int)j);
+                consider_sel(h, tmin, j, ob.key);
+                consider_sel(h, tmax, j, ob.key);
             }
-        } else if (type == 4) {  // groups (598-720)
+        }
+    }
+    if (FL & F_GROUPS) {
+        for (j = S.run_end[3]; j < S.run_end[4]; j++) {  // groups (598-720)
+            const DevObject& ob = S.objs[j];
+            d4 o = xform(ob.inv, ob.st, ro);
+            d4 d = xform(ob.inv, ob.st, rd);
             if (!ray_box(o, d, ob.bb_min, ob.bb_max)) continue;
-            for (int ci = 0; ci < ob.child_count; ci++) walk_group(S, S.roots[ob.child_base + ci], (int)j, o, d, h);
+            for (int ci = 0; ci < ob.child_count; ci++)
+                walk_group(S, S.roots[ob.child_base + ci], j, ob.key, o, d, h);
         }
     }
     return h;
@@ -272,7 +352,8 @@ __device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float
     d4 axis = fabs(nv.x) > 0.1 ? mk(0.0, 1.0, 0.0, 0.0) : mk(1.0, 0.0, 0.0, 0.0);
     d4 u = normalize4(cross4(axis, nv));
     d4 v = cross4(nv, u);
-    double cr = cos(rand1), sr = sin(rand1);
+    double sr, cr;
+    sincos(rand1, &sr, &cr);  // ocml sincos == (sin, cos) bit-for-bit: one shared reduction
     return add4(add4(scl4(scl4(u, cr), rand2s), scl4(scl4(v, sr), rand2s)), scl4(nv, sqrt(1.0 - rand2)));
 }
 
@@ -286,11 +367,14 @@ __device__ __noinline__ void sunflower(int amount, int point, double& ox, double
     double r = 1.0;
     if (idx <= (n - b)) r = sqrt(idx - 0.5) / sqrt(n - (b + 1.0) / 2.0);
     double theta = 2.0 * kPi * idx / (phi * phi);
-    ox = r * cos(theta);
-    oy = r * sin(theta);
+    double st, ct;
+    sincos(theta, &st, &ct);
+    ox = r * ct;
+    oy = r * st;
 }
 
 // rayForPixel (tracer.cl:745-779)
+template <bool kDof>
 __device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, unsigned x, unsigned y, float rx, float ry,
                                               int sample, int total, d4& ro, d4& rd) {
     double xo = cam.pixel_size * ((double)x + (double)rx);
@@ -299,7 +383,7 @@ __device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, unsigned x, 
     d4 pixel = mat_mul(cam.inv, piv);
     d4 origin = mat_mul(cam.inv, mk(0.0, 0.0, 0.0, 1.0));
     d4 dir = normalize4(sub4(pixel, origin));
-    if (cam.aperture != 0) {
+    if (kDof && cam.aperture != 0) {
         d4 pos = add4(origin, scl4(dir, cam.focal_length));
         double sx, sy;
         sunflower(total, sample, sx, sy);
@@ -311,40 +395,65 @@ __device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, unsigned x, 
     rd = dir;
 }
 
-// One path (the body of the sample loop, tracer.cl:867-1179) with the shading
-// reduction (1116-1176) applied as bounces are produced: identical arithmetic,
-// no bounce array.  Returns the path's accumColor.xyz.
-__device__ __forceinline__ void trace_path(const DevScene& S, float fgi, float fgi2, unsigned x, unsigned y,
-                                           uint32_t n, uint32_t samples, double& ar, double& ag, double& ab) {
+// Per-lane path state.  A lane walks its chunk of samples as a sequence of
+// bounce steps; when a path ends it immediately starts its next sample (path
+// regeneration), so lanes of a wave never idle waiting for the wave's longest
+// path.  Within a lane the arithmetic and its order are exactly the reference's
+// sample loop (tracer.cl:867-1179) with the shading reduction (1116-1176)
+// applied as each bounce is produced.
+struct PathState {
     d4 ro, rd;
-    ray_for_pixel(S.cam, x, y, noise3d(fgi, (float)n, fgi2), noise3d(fgi, fgi2, (float)n), (int)n, (int)samples, ro,
-                  rd);
-    double mr = 1.0, mg = 1.0, mb = 1.0;  // mask
-    ar = ag = ab = 0.0;                    // accumColor
-    bool done = false;                     // the reduction has hit its `break`
-    bool inside = false;
-    unsigned effective = 0, k = 0;
-    for (uint32_t b = 0; b < kMaxBounces && effective < kMaxEffectiveBounces; b++) {
-        Hit h = find_closest(S, ro, rd);
-        if (h.obj < 0) break;  // a miss repeats identically until b == 10 in the reference
-        const DevObject& ob = S.objs[h.obj];
-        const int type = ob.type;
-        d4 pos = add4(ro, scl4(rd, h.t));
-        d4 eye = mk(-rd.x, -rd.y, -rd.z, -rd.w);
+    double mr, mg, mb;  // mask
+    double ar, ag, ab;  // accumColor
+    unsigned b, k, effective;
+    bool inside, done;
+    // A camera ray with a NaN component (DoF sample 0: sunflowerRadius(0) =
+    // sqrt(-0.5), tracer.cl:224) makes every object-space component NaN in the
+    // reference (0*NaN = NaN), so it misses everything and the sample adds 0.
+    bool dead;
+};
+
+template <int FL>
+__device__ __forceinline__ void start_path(const DevScene& S, PathState& P, float fgi, float fgi2, unsigned x,
+                                           unsigned y, uint32_t n, uint32_t samples) {
+    ray_for_pixel<(FL & F_DOF) != 0>(S.cam, x, y, noise3d(fgi, (float)n, fgi2), noise3d(fgi, fgi2, (float)n), (int)n,
+                                     (int)samples, P.ro, P.rd);
+    P.mr = P.mg = P.mb = 1.0;
+    P.ar = P.ag = P.ab = 0.0;
+    P.b = P.k = P.effective = 0;
+    P.inside = P.done = false;
+    P.dead = !(isfinite(P.ro.x) && isfinite(P.ro.y) && isfinite(P.ro.z) && isfinite(P.ro.w) && isfinite(P.rd.x) &&
+               isfinite(P.rd.y) && isfinite(P.rd.z) && isfinite(P.rd.w));
+}
+
+// One bounce (tracer.cl:884-1110).  Returns true when the path has ended.
+template <int FL>
+__device__ __forceinline__ bool bounce_step(const DevScene& S, PathState& P, float fgi, uint32_t n) {
+    if (P.dead) return true;
+    Hit h = find_closest<FL>(S, P.ro, P.rd);
+    if (h.obj < 0) return true;  // a miss repeats identically until b == 10 in the reference
+    const DevObject& ob = S.objs[h.obj];
+    const int type = ob.type;
+    const uint32_t b = P.b;
+    d4 pos = add4(P.ro, scl4(P.rd, h.t));
+    d4 eye = mk(-P.rd.x, -P.rd.y, -P.rd.z, -P.rd.w);
+    // Object normal -> world normal (tracer.cl:903-955).
+    d4 nv;
+    if (type == 0) {
+        nv = ld4(ob.plane_n);  // constant per plane: normalize(mul(invT, (0,1,0,0))), w = 0
+    } else {
         d4 on;
-        if (type == 0) {
-            on = mk(0.0, 1.0, 0.0, 0.0);
-        } else if (type == 1) {
-            d4 lp = mat_mul(ob.inv, pos);
+        if (type == 1) {
+            d4 lp = xform(ob.inv, ob.st, pos);
             on = mk(lp.x - 0.0, lp.y - 0.0, lp.z - 0.0, lp.w - 1.0);
-        } else if (type == 2) {
-            d4 lp = mat_mul(ob.inv, pos);
+        } else if ((FL & F_CYLCUBE) && type == 2) {
+            d4 lp = xform(ob.inv, ob.st, pos);
             double dist = lp.x * lp.x + lp.z * lp.z;  // pow(v, 2) folds to v*v
             if (dist < 1 && lp.y >= ob.max_y - kEps) on = mk(0.0, 1.0, 0.0, 0.0);
             else if (dist < 1 && lp.y <= ob.min_y + kEps) on = mk(0.0, -1.0, 0.0, 0.0);
             else on = mk(lp.x, 0.0, lp.z, 0.0);
-        } else if (type == 3) {
-            d4 lp = mat_mul(ob.inv, pos);
+        } else if ((FL & F_CYLCUBE) && type == 3) {
+            d4 lp = xform(ob.inv, ob.st, pos);
             double mc = max3(fabs(lp.x), fabs(lp.y), fabs(lp.z));
             if (mc == fabs(lp.x)) on = mk(lp.x, 0.0, 0.0, 0.0);
             else if (mc == fabs(lp.y)) on = mk(0.0, lp.y, 0.0, 0.0);
@@ -353,86 +462,98 @@ __device__ __forceinline__ void trace_path(const DevScene& S, float fgi, float f
             const DevTriShade& T = S.tri_shade[h.tri];
             on = add4(add4(scl4(ld4(T.n2), h.u), scl4(ld4(T.n3), h.v)), scl4(ld4(T.n1), 1.0 - h.u - h.v));
         }
-        d4 nv = mat_mul(ob.inv_t, on);
-        nv.w = 0.0;
-        nv = normalize4(nv);
-        if (dot4(eye, nv) < 0.0) nv = scl4(nv, -1.0);
-        d4 over = add4(pos, scl4(nv, kEps));
-        double cosine = 1.0;
-        bool entering = false, exiting = false, reflecting = false;
-        // Material decision (tracer.cl:973-1061)
-        if (ob.reflectivity != 0.0 && noise3d(fgi, (float)n, (float)b) < ob.reflectivity) {
-            rd = reflect(rd, nv);
-            reflecting = true;
-        } else if (ob.refractive_index == -1.0) {
-            if (schlick(eye, nv, 1.0, 1.5) < noise3d(fgi, (float)(n * n), (float)b)) {
-                over = sub4(pos, scl4(nv, kEps));
-            } else {
-                rd = reflect(rd, nv);
-                reflecting = true;
-            }
-        } else if (ob.refractive_index != 1.0) {
-            const double ri = ob.refractive_index;
-            const double sch = inside ? schlick(eye, nv, ri, 1.0) : schlick(eye, nv, 1.0, ri);
-            if (sch < noise3d(fgi, (float)(n * n), (float)b)) {
-                rd = inside ? refracted(eye, nv, ri, 1.0) : refracted(eye, nv, 1.0, ri);
-                over = sub4(pos, scl4(nv, kEps));
-                entering = !inside;
-                exiting = inside;
-                inside = !inside;
-            } else {
-                rd = reflect(rd, nv);
-                reflecting = true;
-            }
+        // mul(invT, n) with .w then set to 0: row 3 is dead; diagonal rows 0-2 when invt_diag.
+        const double* it = ob.inv_t;
+        if (ob.invt_diag) {
+            nv = mk(it[0] * on.x, it[5] * on.y, it[10] * on.z, 0.0);
         } else {
-            rd = random_hemisphere(nv, fgi, (float)b, (float)n);
-            cosine = dot4(rd, nv);
+            nv.x = ((it[0] * on.x + it[1] * on.y) + it[2] * on.z) + it[3] * on.w;
+            nv.y = ((it[4] * on.x + it[5] * on.y) + it[6] * on.z) + it[7] * on.w;
+            nv.z = ((it[8] * on.x + it[9] * on.y) + it[10] * on.z) + it[11] * on.w;
+            nv.w = 0.0;
         }
-        ro = over;
-        // Bounce record + reduction step (tracer.cl:1071-1096, 1148-1175).
-        if (!done && !(entering || exiting)) {
-            double er, eg, eb, cr, cg, cb;
-            if (type == 4) {
-                const DevTriShade& T = S.tri_shade[h.tri];
-                er = eg = eb = 0.0;
-                cr = T.color[0];
-                cg = T.color[1];
-                cb = T.color[2];
-            } else {
-                er = ob.emission[0];
-                eg = ob.emission[1];
-                eb = ob.emission[2];
-                cr = ob.color[0];
-                cg = ob.color[1];
-                cb = ob.color[2];
-            }
-            ar = ar + mr * er;
-            ag = ag + mg * eg;
-            ab = ab + mb * eb;
-            if (er > 0.0) {
-                if (k == 0) {
-                    ar = cr;
-                    ag = cg;
-                    ab = cb;
-                }
-                done = true;
-            } else {
-                mr = mr * cr;
-                mg = mg * cg;
-                mb = mb * cb;
-                mr = mr * cosine;
-                mg = mg * cosine;
-                mb = mb * cosine;
-            }
-        }
-        if (!entering && !exiting && !reflecting) effective++;
-        k++;
-        if (ob.emission[0] > 0.0) break;
+        nv = normalize4(nv);
     }
+    if (dot4(eye, nv) < 0.0) nv = scl4(nv, -1.0);
+    d4 over = add4(pos, scl4(nv, kEps));
+    double cosine = 1.0;
+    bool entering = false, exiting = false, reflecting = false;
+    // Material decision (tracer.cl:973-1061)
+    if ((FL & F_MATERIALS) && ob.reflectivity != 0.0 && noise3d(fgi, (float)n, (float)b) < ob.reflectivity) {
+        P.rd = reflect(P.rd, nv);
+        reflecting = true;
+    } else if ((FL & F_MATERIALS) && ob.refractive_index == -1.0) {
+        if (schlick(eye, nv, 1.0, 1.5) < noise3d(fgi, (float)(n * n), (float)b)) {
+            over = sub4(pos, scl4(nv, kEps));
+        } else {
+            P.rd = reflect(P.rd, nv);
+            reflecting = true;
+        }
+    } else if ((FL & F_MATERIALS) && ob.refractive_index != 1.0) {
+        const double ri = ob.refractive_index;
+        const bool in = P.inside;
+        const double sch = in ? schlick(eye, nv, ri, 1.0) : schlick(eye, nv, 1.0, ri);
+        if (sch < noise3d(fgi, (float)(n * n), (float)b)) {
+            P.rd = in ? refracted(eye, nv, ri, 1.0) : refracted(eye, nv, 1.0, ri);
+            over = sub4(pos, scl4(nv, kEps));
+            entering = !in;
+            exiting = in;
+            P.inside = !in;
+        } else {
+            P.rd = reflect(P.rd, nv);
+            reflecting = true;
+        }
+    } else {
+        P.rd = random_hemisphere(nv, fgi, (float)b, (float)n);
+        cosine = dot4(P.rd, nv);
+    }
+    P.ro = over;
+    // Bounce record + reduction step (tracer.cl:1071-1096, 1148-1175).
+    if (!P.done && !(entering || exiting)) {
+        double er, eg, eb, cr, cg, cb;
+        if ((FL & F_GROUPS) && type == 4) {
+            const DevTriShade& T = S.tri_shade[h.tri];
+            er = eg = eb = 0.0;
+            cr = T.color[0];
+            cg = T.color[1];
+            cb = T.color[2];
+        } else {
+            er = ob.emission[0];
+            eg = ob.emission[1];
+            eb = ob.emission[2];
+            cr = ob.color[0];
+            cg = ob.color[1];
+            cb = ob.color[2];
+        }
+        P.ar = P.ar + P.mr * er;
+        P.ag = P.ag + P.mg * eg;
+        P.ab = P.ab + P.mb * eb;
+        if (er > 0.0) {
+            if (P.k == 0) {
+                P.ar = cr;
+                P.ag = cg;
+                P.ab = cb;
+            }
+            P.done = true;
+        } else {
+            P.mr = P.mr * cr;
+            P.mg = P.mg * cg;
+            P.mb = P.mb * cb;
+            P.mr = P.mr * cosine;
+            P.mg = P.mg * cosine;
+            P.mb = P.mb * cosine;
+        }
+    }
+    if (!entering && !exiting && !reflecting) P.effective++;
+    P.k++;
+    P.b = b + 1;
+    // Loop exits of tracer.cl:884 / 1107-1109.
+    return ob.emission[0] > 0.0 || P.b >= kMaxBounces || P.effective >= kMaxEffectiveBounces;
 }
 
 // grid: x = 4 tiles per block (one 8x8 tile per wave), y = sample chunk.
 // Writes the chunk's RGB sums (A = #samples) to out[(chunk*npix + pixel)*4].
+template <int FL>
 __global__ __launch_bounds__(256) void trace_kernel(DevScene S, uint32_t samples, uint32_t s_begin, uint32_t s_end,
                                                     uint32_t chunk_len, uint32_t tile_stride, uint32_t tile_offset,
                                                     const double* __restrict__ seeds, double* __restrict__ out) {
@@ -451,21 +572,49 @@ __global__ __launch_bounds__(256) void trace_kernel(DevScene S, uint32_t samples
     const uint32_t c1 = min(s_end, c0 + chunk_len);
     // fgi / fgi2 (tracer.cl:839-841): double division rounded to float.
     const double seed = seeds[i];
-    const float fgi = (float)(seed / (double)S.n_obj);
+    const float fgi = (float)(seed / (double)S.n_list);
     const float fgi2 = (float)(seed / (double)samples);
     double cr = 0.0, cg = 0.0, cb = 0.0;
-    for (uint32_t n = c0; n < c1; n++) {
-        double ar, ag, ab;
-        trace_path(S, fgi, fgi2, (unsigned)px, (unsigned)py, n, samples, ar, ag, ab);
-        cr = cr + ar;
-        cg = cg + ag;
-        cb = cb + ab;
+    uint32_t n = c0;
+    PathState P;
+    bool need_camera = true;
+    while (n < c1) {
+        if (need_camera) {
+            start_path<FL>(S, P, fgi, fgi2, (unsigned)px, (unsigned)py, n, samples);
+            need_camera = false;
+        }
+        if (bounce_step<FL>(S, P, fgi, n)) {
+            cr = cr + P.ar;  // colors += accumColor (tracer.cl:1179)
+            cg = cg + P.ag;
+            cb = cb + P.ab;
+            n++;
+            need_camera = true;
+        }
     }
     double* o = out + ((size_t)blockIdx.y * ((size_t)W * H) + i) * 4;
     o[0] = cr;
     o[1] = cg;
     o[2] = cb;
     o[3] = (double)(c1 > c0 ? c1 - c0 : 0);
+}
+
+// Per-plane constant world normal: the exact arithmetic of tracer.cl:913, 953-955
+// for objectNormal = (0,1,0,0), done once per scene with the kernel's own math.
+__global__ void plane_normals_kernel(DevObject* objs, int n) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n || objs[j].type != 0) return;
+    d4 nv = mat_mul(objs[j].inv_t, mk(0.0, 1.0, 0.0, 0.0));
+    nv.w = 0.0;
+    nv = normalize4(nv);
+    objs[j].plane_n[0] = nv.x;
+    objs[j].plane_n[1] = nv.y;
+    objs[j].plane_n[2] = nv.z;
+    objs[j].plane_n[3] = nv.w;
+}
+
+hipError_t launch_plane_normals(DevObject* objs, int n, hipStream_t st) {
+    hipLaunchKernelGGL(plane_normals_kernel, dim3(1), dim3(64), 0, st, objs, n);
+    return hipGetLastError();
 }
 
 // Sum chunk partials in chunk order (deterministic); zero un-owned pixels.
@@ -518,15 +667,30 @@ __global__ __launch_bounds__(256) void seeds_kernel(double* __restrict__ seeds, 
 }
 
 // ---- host-side launch wrappers (called from ptmi_api.cpp) ----------------------
-const void* trace_kernel_symbol() { return reinterpret_cast<const void*>(&trace_kernel); }
+const void* trace_kernel_symbol(int flags) {
+    switch (flags & F_ALL) {
+#define K(f) \
+    case f: return reinterpret_cast<const void*>(&trace_kernel<f>);
+        K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15)
+#undef K
+    }
+    return nullptr;
+}
 
-hipError_t launch_trace(const DevScene& S, uint32_t samples, uint32_t s_begin, uint32_t s_end, uint32_t chunk_len,
-                        uint32_t nchunks, uint32_t tile_stride, uint32_t tile_offset, const double* seeds,
-                        double* out, hipStream_t st) {
+hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, uint32_t s_begin, uint32_t s_end,
+                        uint32_t chunk_len, uint32_t nchunks, uint32_t tile_stride, uint32_t tile_offset,
+                        const double* seeds, double* out, hipStream_t st) {
     const int tiles = ((S.cam.width + kTile - 1) / kTile) * ((S.cam.height + kTile - 1) / kTile);
     dim3 grid((tiles + kWavesPerBlock - 1) / kWavesPerBlock, nchunks);
-    hipLaunchKernelGGL(trace_kernel, grid, dim3(256), 0, st, S, samples, s_begin, s_end, chunk_len, tile_stride,
-                       tile_offset, seeds, out);
+    switch (flags & F_ALL) {
+#define K(f)                                                                                                   \
+    case f:                                                                                                    \
+        hipLaunchKernelGGL(trace_kernel<f>, grid, dim3(256), 0, st, S, samples, s_begin, s_end, chunk_len,     \
+                           tile_stride, tile_offset, seeds, out);                                              \
+        break;
+        K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15)
+#undef K
+    }
     return hipGetLastError();
 }
 

@@ -36,6 +36,9 @@ def test_hip_matches_reference_golden(golden_cases, name):
                   float(z["aperture"]), float(z["focal_length"]))
     err = np.abs(out - z["rgba"]).max()
     assert err < TOL, "%s: L-inf %.3e vs reference kernel" % (name, err)
+    # Same device-library math as the reference build: agreement is at the level
+    # of FP64 rounding (any semantic slip moves a pixel by ~1/spp).
+    assert err < 1e-12, "%s: L-inf %.3e (expected rounding-level agreement)" % (name, err)
 
 
 @pytest.mark.parametrize("scene,w,h,spp,ap,fl,seed", [
@@ -55,6 +58,20 @@ def test_hip_matches_live_reference(scene, w, h, spp, ap, fl, seed):
     out = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
     err = np.abs(out - ref).max()
     assert err < TOL, "%s: L-inf %.3e vs live reference" % (scene, err)
+    assert err < 1e-12, "%s: L-inf %.3e (expected rounding-level agreement)" % (scene, err)
+
+
+@pytest.mark.parametrize("scene,ap", [("reference", 0.0), ("default", 0.15), ("teapot", 0.0)])
+def test_generic_instantiation_matches(monkeypatch, scene, ap):
+    """The feature-specialised kernel instantiation and the generic one (all
+    features compiled in, PTMI_FORCE_FLAGS=15) give identical images."""
+    w, h, spp = 40, 24, 3
+    objs, tris, grps, cam = scene_inputs(scene, w, h, ap, 1.6 if ap else 0.0)
+    seeds = layout.seeds_go_float64(w * h, 77)
+    spec = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    monkeypatch.setenv("PTMI_FORCE_FLAGS", "15")
+    gen = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    assert np.array_equal(spec, gen)
 
 
 def test_hip_matches_cpu_oracle_odd_size():
