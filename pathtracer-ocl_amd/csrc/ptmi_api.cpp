@@ -19,7 +19,8 @@
 namespace ptmi {
 hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, uint32_t s_begin, uint32_t s_end,
                         uint32_t chunk_len, uint32_t nchunks, uint32_t tile_stride, uint32_t tile_offset,
-                        const double* seeds, double* out, hipStream_t st);
+                        const double* seeds, const double* sunf, double* out, hipStream_t st);
+hipError_t launch_sunflower(double* out, uint32_t samples, hipStream_t st);
 hipError_t launch_reduce(const double* part, double* sums, uint32_t npix, uint32_t nchunks, int W, int H,
                          uint32_t tile_stride, uint32_t tile_offset, hipStream_t st);
 hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint32_t samples, hipStream_t st);
@@ -35,6 +36,8 @@ struct ptmi_scene {
     DevScene dev{};
     void* buffers[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     double* partial = nullptr;  // chunk partial sums, grown on demand
+    double* sunf = nullptr;     // DoF aperture table for sunf_samples (sunflower_kernel)
+    uint32_t sunf_samples = 0;
     size_t partial_bytes = 0;
     int resident_waves = 0;  // device-wide resident waves of trace_kernel
     uint32_t width = 0, height = 0;
@@ -357,6 +360,7 @@ void ptmi_scene_destroy(ptmi_scene* s) {
     for (void* b : s->buffers)
         if (b) hipFree(b);
     if (s->partial) hipFree(s->partial);
+    if (s->sunf) hipFree(s->sunf);
     for (auto& e : s->events) {
         hipEventDestroy(e.first);
         hipEventDestroy(e.second);
@@ -396,6 +400,16 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     chunks = std::max<uint32_t>(1, std::min<uint32_t>(chunks, std::max<uint32_t>(range, 1)));
     const uint32_t chunk_len = range == 0 ? 1 : (range + chunks - 1) / chunks;
     chunks = range == 0 ? 1 : (range + chunk_len - 1) / chunk_len;
+    if ((s->flags & 8) && s->dev.cam.aperture != 0 && s->sunf_samples != samples) {  // DoF table for this S
+        if (s->sunf) {
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipFree(s->sunf));
+            s->sunf = nullptr;
+        }
+        HIP_TRY(hipMalloc((void**)&s->sunf, (size_t)samples * 2 * sizeof(double)));
+        HIP_TRY(launch_sunflower(s->sunf, samples, st));
+        s->sunf_samples = samples;
+    }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (s->timing) {
         for (hipEvent_t* e : {&ev0, &ev1}) {
@@ -411,7 +425,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         if (tile_stride > 1) HIP_TRY(hipMemsetAsync(sums_dev, 0, (size_t)npix * 4 * sizeof(double), st));
         if (ev0) HIP_TRY(hipEventRecord(ev0, st));
         HIP_TRY(launch_trace(s->dev, s->flags, samples, sample_begin, sample_end, chunk_len, 1, tile_stride, tile_offset,
-                             seeds_dev, sums_dev, st));
+                             seeds_dev, s->sunf, sums_dev, st));
         if (ev1) {
             HIP_TRY(hipEventRecord(ev1, st));
             s->events.emplace_back(ev0, ev1);
@@ -431,7 +445,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     }
     if (ev0) HIP_TRY(hipEventRecord(ev0, st));
     HIP_TRY(launch_trace(s->dev, s->flags, samples, sample_begin, sample_end, chunk_len, chunks, tile_stride, tile_offset,
-                         seeds_dev, s->partial, st));
+                         seeds_dev, s->sunf, s->partial, st));
     if (ev1) {
         HIP_TRY(hipEventRecord(ev1, st));
         s->events.emplace_back(ev0, ev1);

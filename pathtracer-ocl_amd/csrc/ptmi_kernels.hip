@@ -15,12 +15,23 @@
 
 #include "ptmi_device.h"
 
+// PTMI_ABLATE: DIAGNOSTIC builds only (make ablate) -- removes a component to
+// measure its share of the run time.  Images from such builds are wrong by
+// design; the product is always built with PTMI_ABLATE == 0.
+#ifndef PTMI_ABLATE
+#define PTMI_ABLATE 0
+#endif
+
 namespace ptmi {
 
 static constexpr unsigned kMaxEffectiveBounces = 4;  // tracer.cl:2
 static constexpr unsigned kMaxBounces = 10;          // tracer.cl:3
 static constexpr double kEps = 0.0001;               // tracer.cl:4
 static constexpr double kPi = (double)3.14159265359f;  // tracer.cl:1 (a float literal)
+// Camera-ray batch refill policy (trace_kernel): refill when this many lanes
+// have an empty buffer, or this many lanes are idle waiting for a ray.
+static constexpr int kRefillNeed = 24;
+static constexpr int kRefillStarve = 6;
 
 struct d4 {
     double x, y, z, w;
@@ -91,6 +102,10 @@ __device__ __forceinline__ double row1(const double* __restrict__ m, bool st, d4
 
 // noise3D (tracer.cl:314-317): float math, ocml sin_f32, ocml fract_f32.
 __device__ __forceinline__ float noise3d(float x, float y, float z) {
+    if (PTMI_ABLATE & 1) {
+        float v = x * 0.6180339f + y * 0.3473f + z * 0.1234f;
+        return v - floorf(v);
+    }
     float a = x * 112.9898f;
     float b = y * 179.233f;
     float c = z * 237.212f;
@@ -233,11 +248,16 @@ __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int ke
     double c = dot4(vtc, vtc) - 1.0;
     double disc = (b * b) - 4 * a * c;
     if (disc > 0.0) {
+        // a > 0 and sq >= 0 give t1 <= t2 after rounding (rounding is monotonic),
+        // so t2 can only be recorded as the winner when t1 itself is not a
+        // candidate (t1 <= EPSILON); a tie t2 == t1 never replaces t1.
         double sq = sqrt(disc);
         double t1 = (-b - sq) / (2 * a);
-        double t2 = (-b + sq) / (2 * a);
         consider_sel(h, t1, slot, key);
-        consider_sel(h, t2, slot, key);
+        if (!(t1 > kEps)) {
+            double t2 = (-b + sq) / (2 * a);
+            consider_sel(h, t2, slot, key);
+        }
     }
 }
 
@@ -246,14 +266,14 @@ __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int ke
 template <int FL>
 __device__ __forceinline__ Hit find_closest(const DevScene& S, d4 ro, d4 rd) {
     Hit h{1024.0, -1, -1, -1, 0.0, 0.0};
-    for (int p = 0; p < S.n_planes; p++) {  // intersectPlane (478-483): row 1 only
+    for (int p = 0; p < ((PTMI_ABLATE & 8) ? 0 : S.n_planes); p++) {  // intersectPlane (478-483): row 1 only
         const PlaneRec& P = S.planes[p];
         const double oy = ((P.row1[0] * ro.x + P.row1[1] * ro.y) + P.row1[2] * ro.z) + P.row1[3] * ro.w;
         const double dy = ((P.row1[0] * rd.x + P.row1[1] * rd.y) + P.row1[2] * rd.z) + P.row1[3] * rd.w;
         const double q = -oy / dy;
         consider_sel(h, fabs(dy) > kEps ? q : 0.0, P.slot, P.key);
     }
-    for (int q = 0; q < S.n_spheres_st; q++) {  // scale+translate spheres
+    for (int q = 0; q < ((PTMI_ABLATE & 16) ? 0 : S.n_spheres_st); q++) {  // scale+translate spheres
         const SphereRec& Q = S.spheres[q];
         const d4 o = mk(Q.m0 * ro.x + Q.m3 * ro.w, Q.m5 * ro.y + Q.m7 * ro.w, Q.m10 * ro.z + Q.m11 * ro.w,
                         Q.m15 * ro.w);
@@ -349,11 +369,19 @@ __device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float
     double rand1 = 2.0 * kPi * (double)noise3d(fx, fy, fz);
     double rand2 = (double)noise3d(fy, fz, fx);
     double rand2s = sqrt(rand2);
-    d4 axis = fabs(nv.x) > 0.1 ? mk(0.0, 1.0, 0.0, 0.0) : mk(1.0, 0.0, 0.0, 0.0);
-    d4 u = normalize4(cross4(axis, nv));
+    // cross(axis, n) for a unit axis: the fma chains of opencl.bc's cross reduce
+    // exactly (up to the sign of exact zeros) to component moves:
+    //   cross((0,1,0,0), n) = (n.z, 0, -n.x, 0),  cross((1,0,0,0), n) = (0, -n.z, n.y, 0)
+    d4 c = fabs(nv.x) > 0.1 ? mk(nv.z, 0.0, -nv.x, 0.0) : mk(0.0, -nv.z, nv.y, 0.0);
+    d4 u = normalize4(c);
     d4 v = cross4(nv, u);
     double sr, cr;
-    sincos(rand1, &sr, &cr);  // ocml sincos == (sin, cos) bit-for-bit: one shared reduction
+    if (PTMI_ABLATE & 4) {
+        cr = 1.0 - rand1 * 0.1;
+        sr = rand1 * 0.15;
+    } else {
+        sincos(rand1, &sr, &cr);  // ocml sincos == (sin, cos) bit-for-bit: one shared reduction
+    }
     return add4(add4(scl4(scl4(u, cr), rand2s), scl4(scl4(v, sr), rand2s)), scl4(nv, sqrt(1.0 - rand2)));
 }
 
@@ -373,20 +401,43 @@ __device__ __noinline__ void sunflower(int amount, int point, double& ox, double
     oy = r * st;
 }
 
-// rayForPixel (tracer.cl:745-779)
+// Per-frame camera constants (computed once per thread from the uniform camera
+// record; exact rewrites of the reference's rayForPixel arithmetic):
+//   origin = mul(inverse, (0,0,0,1))                      -- a frame constant
+//   pixel  = mul(inverse, (hw - xo, hh - yo, -1, 1)) where m*(-1) == -m and
+//            m*1 == m exactly, so row r = ((m0 a + m1 b) + (-m2)) + m3.
+struct CamConst {
+    d4 origin;
+    double nm2[4], m3[4];
+};
+__device__ __forceinline__ CamConst cam_const(const DevCamera& cam) {
+    CamConst c;
+    c.origin = mat_mul(cam.inv, mk(0.0, 0.0, 0.0, 1.0));
+    for (int r = 0; r < 4; r++) {
+        c.nm2[r] = -cam.inv[4 * r + 2];
+        c.m3[r] = cam.inv[4 * r + 3];
+    }
+    return c;
+}
+
+// rayForPixel (tracer.cl:745-779).  With DoF the aperture offset
+// sunflower(S, 2, n) depends only on n: it is read from a per-frame table
+// (sunflower_kernel) made with the same arithmetic.
 template <bool kDof>
-__device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, unsigned x, unsigned y, float rx, float ry,
-                                              int sample, int total, d4& ro, d4& rd) {
+__device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, const CamConst& cc, const double* __restrict__ sunf,
+                                              unsigned x, unsigned y, float rx, float ry, int sample, d4& ro,
+                                              d4& rd) {
     double xo = cam.pixel_size * ((double)x + (double)rx);
     double yo = cam.pixel_size * ((double)y + (double)ry);
-    d4 piv = mk(cam.half_width - xo, cam.half_height - yo, -1.0, 1.0);
-    d4 pixel = mat_mul(cam.inv, piv);
-    d4 origin = mat_mul(cam.inv, mk(0.0, 0.0, 0.0, 1.0));
-    d4 dir = normalize4(sub4(pixel, origin));
+    const double a = cam.half_width - xo, b = cam.half_height - yo;
+    const double* m = cam.inv;
+    d4 pixel = mk(((m[0] * a + m[1] * b) + cc.nm2[0]) + cc.m3[0], ((m[4] * a + m[5] * b) + cc.nm2[1]) + cc.m3[1],
+                  ((m[8] * a + m[9] * b) + cc.nm2[2]) + cc.m3[2], ((m[12] * a + m[13] * b) + cc.nm2[3]) + cc.m3[3]);
+    d4 origin = cc.origin;
+    d4 dir = (PTMI_ABLATE & 2) ? sub4(pixel, origin) : normalize4(sub4(pixel, origin));
     if (kDof && cam.aperture != 0) {
         d4 pos = add4(origin, scl4(dir, cam.focal_length));
-        double sx, sy;
-        sunflower(total, sample, sx, sy);
+        const double sx = sunf[2 * sample], sy = sunf[2 * sample + 1];
         d4 no = mk(origin.x + (sy * cam.aperture), origin.y + (sx * cam.aperture), origin.z, 1.0);
         dir = sub4(pos, no);
         origin = no;
@@ -413,17 +464,15 @@ struct PathState {
     bool dead;
 };
 
-template <int FL>
-__device__ __forceinline__ void start_path(const DevScene& S, PathState& P, float fgi, float fgi2, unsigned x,
-                                           unsigned y, uint32_t n, uint32_t samples) {
-    ray_for_pixel<(FL & F_DOF) != 0>(S.cam, x, y, noise3d(fgi, (float)n, fgi2), noise3d(fgi, fgi2, (float)n), (int)n,
-                                     (int)samples, P.ro, P.rd);
+__device__ __forceinline__ void start_path(PathState& P, d4 ro, d4 rd) {
+    P.ro = ro;
+    P.rd = rd;
     P.mr = P.mg = P.mb = 1.0;
     P.ar = P.ag = P.ab = 0.0;
     P.b = P.k = P.effective = 0;
     P.inside = P.done = false;
-    P.dead = !(isfinite(P.ro.x) && isfinite(P.ro.y) && isfinite(P.ro.z) && isfinite(P.ro.w) && isfinite(P.rd.x) &&
-               isfinite(P.rd.y) && isfinite(P.rd.z) && isfinite(P.rd.w));
+    P.dead = !(isfinite(ro.x) && isfinite(ro.y) && isfinite(ro.z) && isfinite(ro.w) && isfinite(rd.x) &&
+               isfinite(rd.y) && isfinite(rd.z) && isfinite(rd.w));
 }
 
 // One bounce (tracer.cl:884-1110).  Returns true when the path has ended.
@@ -554,9 +603,10 @@ __device__ __forceinline__ bool bounce_step(const DevScene& S, PathState& P, flo
 // grid: x = 4 tiles per block (one 8x8 tile per wave), y = sample chunk.
 // Writes the chunk's RGB sums (A = #samples) to out[(chunk*npix + pixel)*4].
 template <int FL>
-__global__ __launch_bounds__(256) void trace_kernel(DevScene S, uint32_t samples, uint32_t s_begin, uint32_t s_end,
+__global__ __launch_bounds__(256, (FL & F_GROUPS) ? 2 : 4) void trace_kernel(DevScene S, uint32_t samples, uint32_t s_begin, uint32_t s_end,
                                                     uint32_t chunk_len, uint32_t tile_stride, uint32_t tile_offset,
-                                                    const double* __restrict__ seeds, double* __restrict__ out) {
+                                                    const double* __restrict__ seeds, const double* __restrict__ sunf,
+                                                    double* __restrict__ out) {
     const int W = S.cam.width, H = S.cam.height;
     const int tiles_x = (W + kTile - 1) / kTile;
     const int tiles_y = (H + kTile - 1) / kTile;
@@ -575,20 +625,48 @@ __global__ __launch_bounds__(256) void trace_kernel(DevScene S, uint32_t samples
     const float fgi = (float)(seed / (double)S.n_list);
     const float fgi2 = (float)(seed / (double)samples);
     double cr = 0.0, cg = 0.0, cb = 0.0;
-    uint32_t n = c0;
+    const CamConst cc = cam_const(S.cam);
+    // Camera rays are produced in wave-wide batches into a one-deep per-lane
+    // buffer (LDS) and consumed by path regeneration: generating them at the
+    // moment each lane needs one would run the camera block (2 noise3D + the
+    // transform) on nearly every bounce iteration with ~1/5 of the lanes active.
+    // Per lane the samples are still traced in order n = c0, c0+1, ..., so the
+    // arithmetic and the order of `colors +=` are unchanged.
+    __shared__ d4 cam_ro[256], cam_rd[256];
+    const int tid = threadIdx.x;
+    uint32_t n_gen = c0;  // next sample whose camera ray is to be generated
+    uint32_t n_buf = 0, n_cur = 0;
+    bool buf = false, active = false;
     PathState P;
-    bool need_camera = true;
-    while (n < c1) {
-        if (need_camera) {
-            start_path<FL>(S, P, fgi, fgi2, (unsigned)px, (unsigned)py, n, samples);
-            need_camera = false;
+    for (;;) {
+        if (!__any(active || buf || n_gen < c1)) break;
+        const bool need = !buf && n_gen < c1;
+        const int n_need = __popcll(__ballot(need));
+        const int n_starve = __popcll(__ballot(need && !active));
+        if (n_need >= kRefillNeed || n_starve >= kRefillStarve || (n_starve > 0 && !__any(active))) {
+            if (need) {
+                d4 ro, rd;
+                ray_for_pixel<(FL & F_DOF) != 0>(S.cam, cc, sunf, (unsigned)px, (unsigned)py,
+                                                 noise3d(fgi, (float)n_gen, fgi2), noise3d(fgi, fgi2, (float)n_gen),
+                                                 (int)n_gen, ro, rd);
+                cam_ro[tid] = ro;
+                cam_rd[tid] = rd;
+                n_buf = n_gen;
+                n_gen++;
+                buf = true;
+            }
         }
-        if (bounce_step<FL>(S, P, fgi, n)) {
+        if (!active && buf) {
+            start_path(P, cam_ro[tid], cam_rd[tid]);
+            n_cur = n_buf;
+            buf = false;
+            active = true;
+        }
+        if (active && bounce_step<FL>(S, P, fgi, n_cur)) {
             cr = cr + P.ar;  // colors += accumColor (tracer.cl:1179)
             cg = cg + P.ag;
             cb = cb + P.ab;
-            n++;
-            need_camera = true;
+            active = false;
         }
     }
     double* o = out + ((size_t)blockIdx.y * ((size_t)W * H) + i) * 4;
@@ -596,6 +674,22 @@ __global__ __launch_bounds__(256) void trace_kernel(DevScene S, uint32_t samples
     o[1] = cg;
     o[2] = cb;
     o[3] = (double)(c1 > c0 ? c1 - c0 : 0);
+}
+
+// DoF aperture offsets sunflower(S, 2, n) for n in [0, S) (tracer.cl:221-248,
+// 766): a per-frame table, same arithmetic as the reference.
+__global__ void sunflower_kernel(double* __restrict__ out, uint32_t samples) {
+    const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= samples) return;
+    double sx, sy;
+    sunflower((int)samples, (int)n, sx, sy);
+    out[2 * n] = sx;
+    out[2 * n + 1] = sy;
+}
+
+hipError_t launch_sunflower(double* out, uint32_t samples, hipStream_t st) {
+    hipLaunchKernelGGL(sunflower_kernel, dim3((samples + 255) / 256), dim3(256), 0, st, out, samples);
+    return hipGetLastError();
 }
 
 // Per-plane constant world normal: the exact arithmetic of tracer.cl:913, 953-955
@@ -679,14 +773,14 @@ const void* trace_kernel_symbol(int flags) {
 
 hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, uint32_t s_begin, uint32_t s_end,
                         uint32_t chunk_len, uint32_t nchunks, uint32_t tile_stride, uint32_t tile_offset,
-                        const double* seeds, double* out, hipStream_t st) {
+                        const double* seeds, const double* sunf, double* out, hipStream_t st) {
     const int tiles = ((S.cam.width + kTile - 1) / kTile) * ((S.cam.height + kTile - 1) / kTile);
     dim3 grid((tiles + kWavesPerBlock - 1) / kWavesPerBlock, nchunks);
     switch (flags & F_ALL) {
 #define K(f)                                                                                                   \
     case f:                                                                                                    \
         hipLaunchKernelGGL(trace_kernel<f>, grid, dim3(256), 0, st, S, samples, s_begin, s_end, chunk_len,     \
-                           tile_stride, tile_offset, seeds, out);                                              \
+                           tile_stride, tile_offset, seeds, sunf, out);                                        \
         break;
         K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15)
 #undef K
