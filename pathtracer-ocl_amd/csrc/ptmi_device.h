@@ -37,20 +37,37 @@ struct alignas(16) DevObject {
     int32_t pad[2];
 };
 
+// Reference BVH node (CLGroup, tracer.cl:24-35).  Its exact line-box test is
+// the gate that decides which triangles are candidates, as in the reference.
 struct alignas(16) DevNode {
     double bb_min[3];
     double bb_max[3];
-    int32_t tri_offset, tri_count;
     int32_t child0, child1;  // > 0 means present (tracer.cl:683, 704)
+    int32_t local;           // root of this node's triangle sub-BVH (LocalNode index), -1: no triangles
+    int32_t pad;
 };
 static_assert(sizeof(DevNode) == 64, "DevNode must stay 64 B");
 
-struct alignas(16) DevTri {
-    double p1[4];
-    double e1[4];
-    double e2[4];
+// Sub-BVH over ONE reference node's triangle list (built on the host): boxes are
+// the triangles' bounds expanded by a conservative margin, so a ray that misses
+// a LocalNode box cannot produce a Moller-Trumbore hit inside it.
+struct alignas(16) LocalNode {
+    double bb_min[3];
+    double bb_max[3];
+    int32_t left, right;     // children (LocalNode indices), left < 0: leaf
+    int32_t first, count;    // leaf: triangles [first, first + count) of DevScene::tris
 };
-static_assert(sizeof(DevTri) == 96, "DevTri must stay 96 B");
+static_assert(sizeof(LocalNode) == 64, "LocalNode must stay 64 B");
+
+// Triangle in sub-BVH leaf order; `n` is its index in the reference's triangle
+// list (tie-break order and DevTriShade slot).
+struct alignas(16) DevTri {
+    double p1[3];
+    double e1[3];
+    double e2[3];
+    int32_t n, pad;
+};
+static_assert(sizeof(DevTri) == 80, "DevTri must stay 80 B");
 
 struct alignas(16) DevTriShade {
     double n1[4], n2[4], n3[4];
@@ -89,6 +106,7 @@ struct DevScene {
     int32_t pad1;
     const int32_t* roots;  // concatenated group roots of all type-4 objects
     const DevNode* nodes;
+    const LocalNode* lnodes;
     const DevTri* tris;
     const DevTriShade* tri_shade;
     uint32_t n_obj;   // intersectable objects in objs[]

@@ -156,65 +156,19 @@ struct Hit {
 __device__ __forceinline__ bool better(const Hit& h, double t, int key) {
     return t > kEps && (t < h.t || (t == h.t && key < h.key));
 }
+// Triangles of one group object are recorded by the reference in increasing
+// triangle index (nodes are numbered, and their triangles appended, in the same
+// preorder the walk follows: scene.go:96-155, tracer.cl:621-719), so a tie in
+// (t, object) is broken by the triangle index.
+__device__ __forceinline__ bool better_tri(const Hit& h, double t, int key, int tri) {
+    return t > kEps && (t < h.t || (t == h.t && (key < h.key || (key == h.key && tri < h.tri))));
+}
 __device__ __forceinline__ void consider(Hit& h, double t, int obj, int key) {
     if (better(h, t, key)) {
         h.t = t;
         h.obj = obj;
         h.key = key;
         h.tri = -1;
-    }
-}
-
-// Stack-based BVH walk of one group root, in the reference's preorder
-// (tracer.cl:621-719), Moller-Trumbore per triangle (640-675).
-__device__ __noinline__ void walk_group(const DevScene& S, int root, int obj, int key, d4 o, d4 d, Hit& h) {
-    int stack[64];
-    int sidx = 0;
-    int cur_idx = root;
-    const DevNode* cur = &S.nodes[cur_idx];
-    for (;;) {
-        while (cur && ray_box(o, d, cur->bb_min, cur->bb_max)) {
-            const int end = cur->tri_offset + cur->tri_count;
-            for (int n = cur->tri_offset; n < end; n++) {
-                const DevTri& T = S.tris[n];
-                const d4 e1 = ld4(T.e1), e2 = ld4(T.e2);
-                d4 dce2 = cross4(d, e2);
-                double det = dot4(e1, dce2);
-                if (fabs(det) < kEps) continue;
-                double f = 1.0 / det;
-                d4 p1o = sub4(o, ld4(T.p1));
-                double u = f * dot4(p1o, dce2);
-                if (u < 0 || u > 1) continue;
-                d4 oce1 = cross4(p1o, e1);
-                double v = f * dot4(d, oce1);
-                if (v < 0 || (u + v) > 1) continue;
-                double t = f * dot4(e2, oce1);
-                if (better(h, t, key)) {
-                    h.t = t;
-                    h.obj = obj;
-                    h.key = key;
-                    h.tri = n;
-                    h.u = u;
-                    h.v = v;
-                }
-            }
-            stack[sidx++] = cur_idx;
-            if (cur->child0 > 0) {
-                cur_idx = cur->child0;
-                cur = &S.nodes[cur_idx];
-            } else {
-                cur = nullptr;
-            }
-        }
-        sidx--;
-        if (sidx == -1) break;
-        cur = &S.nodes[stack[sidx]];
-        if (cur->child1 > 0) {
-            cur_idx = cur->child1;
-            cur = &S.nodes[cur_idx];
-        } else {
-            cur = nullptr;
-        }
     }
 }
 
@@ -229,6 +183,178 @@ enum : int {
     F_DOF = 8,        // camera aperture != 0
     F_ALL = 15
 };
+
+// intersectRayWithBox (tracer.cl:270-280) returning the line's slab interval.
+// The hit decision tmin < tmax is the reference's, bit for bit.
+__device__ __forceinline__ bool ray_box_t(d4 o, d4 d, const double* mn, const double* mx, double& tmin,
+                                          double& tmax) {
+    double x0, x1, y0, y1, z0, z1;
+    check_axis(o.x, d.x, mn[0], mx[0], x0, x1);
+    check_axis(o.y, d.y, mn[1], mx[1], y0, y1);
+    check_axis(o.z, d.z, mn[2], mx[2], z0, z1);
+    tmin = max3(x0, y0, z0);
+    tmax = min3(x1, y1, z1);
+    return tmin < tmax;
+}
+
+// Conservative slack for pruning by t: computed Moller-Trumbore t values and
+// slab bounds each carry ~1e-16 relative rounding error (~1e-12 absolute at the
+// reference's det >= 1e-4); 1e-9 (1 + t) is orders of magnitude larger.
+__device__ __forceinline__ double prune_margin(double t) { return 1e-9 * (1.0 + fabs(t)); }
+
+// One slab of intersectRayWithBox evaluated with the ray's reciprocal instead of
+// the reference's division: |a*r - RN(a/d)| <= 3u|a/d| (u = 2^-53), bounded here
+// by e = 2^-50 |a*r| + tiny.  Axes with |d| < EPSILON are computed exactly as the
+// reference does (a * +inf, possibly NaN) with e = 0.
+__device__ __forceinline__ void slab_fast(double o, double d, double r, double mn, double mx, double& lo,
+                                          double& hi, double& e) {
+    const double a0 = mn - o, a1 = mx - o;
+    const bool big = fabs(d) >= kEps;
+    const double a = big ? a0 * r : a0 * __builtin_huge_val();
+    const double b = big ? a1 * r : a1 * __builtin_huge_val();
+    lo = a > b ? b : a;  // the reference's swap (tracer.cl:263-266)
+    hi = a > b ? a : b;
+    e = big ? fmax(fabs(a), fabs(b)) * 0x1p-50 + 0x1p-1000 : 0.0;
+}
+
+// intersectRayWithBox (tracer.cl:270-280), decision bit-identical to ray_box_t:
+// interval bounds on the reference's tmin = max(x0,y0,z0), tmax = min(x1,y1,z1)
+// decide almost every box; only boxes within rounding distance of the decision
+// boundary (or with non-finite bounds) are recomputed with the exact divisions.
+// [tlo, thi] bound the reference's (tmin, tmax) for pruning.
+__device__ __forceinline__ bool ray_box_ref(d4 o, d4 d, d4 r, const double* mn, const double* mx, double& tlo,
+                                            double& thi) {
+    double xl, xh, xe, yl, yh, ye, zl, zh, ze;
+    slab_fast(o.x, d.x, r.x, mn[0], mx[0], xl, xh, xe);
+    slab_fast(o.y, d.y, r.y, mn[1], mx[1], yl, yh, ye);
+    slab_fast(o.z, d.z, r.z, mn[2], mx[2], zl, zh, ze);
+    const double t0lo = max3(xl - xe, yl - ye, zl - ze), t0hi = max3(xl + xe, yl + ye, zl + ze);
+    const double t1lo = min3(xh - xe, yh - ye, zh - ze), t1hi = min3(xh + xe, yh + ye, zh + ze);
+    tlo = t0lo;
+    thi = t1hi;
+    if (t0hi < t1lo) return true;    // every tmin <= t0hi < t1lo <= every tmax
+    if (t0lo >= t1hi) return false;  // every tmin >= t0lo >= t1hi >= every tmax
+    double a, b;                     // undecided (or NaN bounds): the reference's arithmetic
+    const bool hit = ray_box_t(o, d, mn, mx, a, b);
+    tlo = a;
+    thi = b;
+    return hit;
+}
+
+// Moller-Trumbore (tracer.cl:640-675) on the 3 live components: the w terms of
+// the reference's dot() products multiply a cross() result whose w is exactly 0.
+__device__ __forceinline__ void tri_test(const DevTri& T, d4 o, d4 d, int slot, int key, Hit& h) {
+    const double e1x = T.e1[0], e1y = T.e1[1], e1z = T.e1[2];
+    const double e2x = T.e2[0], e2y = T.e2[1], e2z = T.e2[2];
+    // dirCrossE2 = cross(d, e2)
+    const double cx = fma(d.y, e2z, e2y * -d.z), cy = fma(d.z, e2x, e2z * -d.x), cz = fma(d.x, e2y, e2x * -d.y);
+    double det = e1x * cx;
+    det = fma(e1y, cy, det);
+    det = fma(e1z, cz, det);
+    if (fabs(det) < kEps) return;
+    const double px = o.x - T.p1[0], py = o.y - T.p1[1], pz = o.z - T.p1[2];
+    double du = px * cx;
+    du = fma(py, cy, du);
+    du = fma(pz, cz, du);
+    // u = (1/det) * du.  Reject before the reciprocal when the sign alone (u < 0)
+    // or |du| >= 2|det| (u > 1 after rounding) decides it.
+    if ((du < 0.0) != (det < 0.0) && du != 0.0) return;
+    if (fabs(du) >= 2.0 * fabs(det)) return;
+    const double f = 1.0 / det;
+    const double u = f * du;
+    if (u < 0 || u > 1) return;
+    // originCrossE1 = cross(p1ToOrigin, e1)
+    const double qx = fma(py, e1z, e1y * -pz), qy = fma(pz, e1x, e1z * -px), qz = fma(px, e1y, e1x * -py);
+    double dv = d.x * qx;
+    dv = fma(d.y, qy, dv);
+    dv = fma(d.z, qz, dv);
+    const double v = f * dv;
+    if (v < 0 || (u + v) > 1) return;
+    double dt = e2x * qx;
+    dt = fma(e2y, qy, dt);
+    dt = fma(e2z, qz, dt);
+    const double t = f * dt;
+    const int n = T.n;
+    if (better_tri(h, t, key, n)) {
+        h.t = t;
+        h.obj = slot;
+        h.key = key;
+        h.tri = n;
+        h.u = u;
+        h.v = v;
+    }
+}
+
+static constexpr int kStack = 48;  // per-lane LDS traversal stack (host checks the bound)
+
+// Stack entries: >= 0 a reference node, <= -2 the sub-BVH node -(e + 2).
+__device__ __forceinline__ int enc_local(int i) { return -(i + 2); }
+
+// BVH walk of one group root.
+//  * Reference nodes gate exactly as in the reference (same line-box decision,
+//    ray_box_ref), so the set of candidate triangles is the reference's; nodes
+//    whose box cannot hold a winning t are skipped (prune_margin).
+//  * A passed node's own triangles are reached through its sub-BVH, whose boxes
+//    are the triangles' bounds widened by 1e-7 x scene scale: a ray that misses
+//    such a box by the slab test below cannot yield a Moller-Trumbore hit inside
+//    it (the computed hit point is within ~1e-15 relative of the triangle).
+//  * Ties resolve through better_tri (triangle index), so the winner is the
+//    reference's whatever the visiting order.
+__device__ __forceinline__ void walk_group(const DevScene& S, int* __restrict__ stk, int root, int slot, int key,
+                                           d4 o, d4 d, d4 r, Hit& h) {
+    int sp = 0;
+    stk[(sp++) * 256] = root;
+    while (sp > 0) {
+        const int e = stk[(--sp) * 256];
+        if (e >= 0) {
+            const DevNode& N = S.nodes[e];
+            double tlo, thi;
+            if (!ray_box_ref(o, d, r, N.bb_min, N.bb_max, tlo, thi)) continue;
+            if (tlo > h.t + prune_margin(h.t) || thi + prune_margin(thi) < kEps) continue;
+            const int c0 = N.child0, c1 = N.child1;
+            if (c0 > 0 && c1 > 0) {
+                // near child visited first: order by box centre along the ray
+                const DevNode& A = S.nodes[c0];
+                const DevNode& B = S.nodes[c1];
+                const double ka = (A.bb_min[0] + A.bb_max[0]) * d.x + (A.bb_min[1] + A.bb_max[1]) * d.y +
+                                  (A.bb_min[2] + A.bb_max[2]) * d.z;
+                const double kb = (B.bb_min[0] + B.bb_max[0]) * d.x + (B.bb_min[1] + B.bb_max[1]) * d.y +
+                                  (B.bb_min[2] + B.bb_max[2]) * d.z;
+                const bool a_first = ka <= kb;
+                stk[(sp++) * 256] = a_first ? c1 : c0;
+                stk[(sp++) * 256] = a_first ? c0 : c1;
+            } else if (c0 > 0) {
+                stk[(sp++) * 256] = c0;
+            } else if (c1 > 0) {
+                stk[(sp++) * 256] = c1;
+            }
+            if (N.local >= 0) stk[(sp++) * 256] = enc_local(N.local);  // own triangles first
+        } else {
+            const LocalNode& L = S.lnodes[-e - 2];
+            const double ax = (L.bb_min[0] - o.x) * r.x, bx = (L.bb_max[0] - o.x) * r.x;
+            const double ay = (L.bb_min[1] - o.y) * r.y, by = (L.bb_max[1] - o.y) * r.y;
+            const double az = (L.bb_min[2] - o.z) * r.z, bz = (L.bb_max[2] - o.z) * r.z;
+            const double tn = max3(fmin(ax, bx), fmin(ay, by), fmin(az, bz));
+            const double tf = min3(fmax(ax, bx), fmax(ay, by), fmax(az, bz));
+            // (NaN bounds -- a NaN ray -- fail every test below: the node is visited.)
+            if (tn > tf || tn > h.t + prune_margin(h.t) || tf + prune_margin(tf) < kEps) continue;
+            if (L.left < 0) {
+                const int end = L.first + L.count;
+                for (int i = L.first; i < end; i++) tri_test(S.tris[i], o, d, slot, key, h);
+            } else {
+                const LocalNode& A = S.lnodes[L.left];
+                const LocalNode& B = S.lnodes[L.right];
+                const double ka = (A.bb_min[0] + A.bb_max[0]) * d.x + (A.bb_min[1] + A.bb_max[1]) * d.y +
+                                  (A.bb_min[2] + A.bb_max[2]) * d.z;
+                const double kb = (B.bb_min[0] + B.bb_max[0]) * d.x + (B.bb_min[1] + B.bb_max[1]) * d.y +
+                                  (B.bb_min[2] + B.bb_max[2]) * d.z;
+                const bool a_first = ka <= kb;
+                stk[(sp++) * 256] = enc_local(a_first ? L.right : L.left);
+                stk[(sp++) * 256] = enc_local(a_first ? L.left : L.right);
+            }
+        }
+    }
+}
 
 // Candidate update as selects (no exec-mask branching).  t > EPSILON implies
 // the reference's `t != 0.0` recording test.
@@ -264,7 +390,7 @@ __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int ke
 // findClosestIntersection (tracer.cl:537-742), one loop per object type.  Loop
 // indices are wave-uniform, so object data arrives through scalar loads.
 template <int FL>
-__device__ __forceinline__ Hit find_closest(const DevScene& S, d4 ro, d4 rd) {
+__device__ __forceinline__ Hit find_closest(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd) {
     Hit h{1024.0, -1, -1, -1, 0.0, 0.0};
     for (int p = 0; p < ((PTMI_ABLATE & 8) ? 0 : S.n_planes); p++) {  // intersectPlane (478-483): row 1 only
         const PlaneRec& P = S.planes[p];
@@ -330,9 +456,12 @@ __device__ __forceinline__ Hit find_closest(const DevScene& S, d4 ro, d4 rd) {
             const DevObject& ob = S.objs[j];
             d4 o = xform(ob.inv, ob.st, ro);
             d4 d = xform(ob.inv, ob.st, rd);
-            if (!ray_box(o, d, ob.bb_min, ob.bb_max)) continue;
+            const d4 r = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z, 0.0);
+            double tmin, tmax;
+            if (!ray_box_ref(o, d, r, ob.bb_min, ob.bb_max, tmin, tmax)) continue;
+            if (tmin > h.t + prune_margin(h.t) || tmax + prune_margin(tmax) < kEps) continue;
             for (int ci = 0; ci < ob.child_count; ci++)
-                walk_group(S, S.roots[ob.child_base + ci], j, ob.key, o, d, h);
+                walk_group(S, stk, S.roots[ob.child_base + ci], j, ob.key, o, d, r, h);
         }
     }
     return h;
@@ -477,9 +606,10 @@ __device__ __forceinline__ void start_path(PathState& P, d4 ro, d4 rd) {
 
 // One bounce (tracer.cl:884-1110).  Returns true when the path has ended.
 template <int FL>
-__device__ __forceinline__ bool bounce_step(const DevScene& S, PathState& P, float fgi, uint32_t n) {
+__device__ __forceinline__ bool bounce_step(const DevScene& S, int* __restrict__ stk, PathState& P, float fgi,
+                                            uint32_t n) {
     if (P.dead) return true;
-    Hit h = find_closest<FL>(S, P.ro, P.rd);
+    Hit h = find_closest<FL>(S, stk, P.ro, P.rd);
     if (h.obj < 0) return true;  // a miss repeats identically until b == 10 in the reference
     const DevObject& ob = S.objs[h.obj];
     const int type = ob.type;
@@ -634,6 +764,10 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? 2 : 4) void trace_kernel(Dev
     // arithmetic and the order of `colors +=` are unchanged.
     __shared__ d4 cam_ro[256], cam_rd[256];
     const int tid = threadIdx.x;
+    // Per-lane BVH traversal stacks, lane-interleaved (entry k of lane t at
+    // [k * 256 + t]) so a wave's pushes and pops hit 64 consecutive dwords.
+    __shared__ int stk_lds[(FL & F_GROUPS) ? kStack * 256 : 1];
+    int* stk = (FL & F_GROUPS) ? stk_lds + tid : nullptr;
     uint32_t n_gen = c0;  // next sample whose camera ray is to be generated
     uint32_t n_buf = 0, n_cur = 0;
     bool buf = false, active = false;
@@ -662,7 +796,7 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? 2 : 4) void trace_kernel(Dev
             buf = false;
             active = true;
         }
-        if (active && bounce_step<FL>(S, P, fgi, n_cur)) {
+        if (active && bounce_step<FL>(S, stk, P, fgi, n_cur)) {
             cr = cr + P.ar;  // colors += accumColor (tracer.cl:1179)
             cg = cg + P.ag;
             cb = cb + P.ab;

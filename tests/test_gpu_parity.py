@@ -47,6 +47,9 @@ def test_hip_matches_reference_golden(golden_cases, name):
     ("default", 64, 64, 6, 0.0, 0.0, 103),
     ("teapot", 48, 32, 3, 0.0, 0.0, 104),
     ("gopher", 48, 32, 2, 0.0, 0.0, 105),
+    ("teapot", 128, 96, 4, 0.0, 0.0, 106),
+    ("gopher", 128, 96, 3, 0.0, 0.0, 107),
+    ("teapot", 96, 64, 3, 0.15, 1.6, 108),
 ])
 def test_hip_matches_live_reference(scene, w, h, spp, ap, fl, seed):
     if not pyoracle.ref_available():
