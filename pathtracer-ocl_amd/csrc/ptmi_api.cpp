@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/ptmi.h"
+#include "ptmi_bvh.h"
 #include "ptmi_device.h"
 
 namespace ptmi {
@@ -35,7 +36,7 @@ using namespace ptmi;
 struct ptmi_scene {
     int device = 0;
     DevScene dev{};
-    void* buffers[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    void* buffers[10] = {};
     double* partial = nullptr;  // chunk partial sums, grown on demand
     double* sunf = nullptr;     // DoF aperture table for sunf_samples (sunflower_kernel)
     uint32_t sunf_samples = 0;
@@ -112,96 +113,9 @@ bool is_diag3(const double* m) {  // rows 0-2 diagonal (row 3 unused)
     return true;
 }
 
-// Bounds of a triangle from the reference record: p1, p2, p3 and the p1+e1,
-// p1+e2 the kernel's Moller-Trumbore actually spans (tracer.cl:640-675).
-void tri_bounds(const uint8_t* b, double mn[3], double mx[3]) {
-    double p[5][3];
-    for (int k = 0; k < 3; k++) {
-        p[0][k] = rd<double>(b + 0 + 8 * k);
-        p[1][k] = rd<double>(b + 32 + 8 * k);
-        p[2][k] = rd<double>(b + 64 + 8 * k);
-        p[3][k] = p[0][k] + rd<double>(b + 96 + 8 * k);
-        p[4][k] = p[0][k] + rd<double>(b + 128 + 8 * k);
-    }
-    for (int k = 0; k < 3; k++) {
-        mn[k] = mx[k] = p[0][k];
-        for (int i = 1; i < 5; i++) {
-            mn[k] = std::min(mn[k], p[i][k]);
-            mx[k] = std::max(mx[k], p[i][k]);
-        }
-    }
-}
-
-int build_local_rec(const uint8_t* tris, std::vector<int32_t>& idx, int lo, int hi, std::vector<LocalNode>& ln,
-                    std::vector<DevTri>& ht) {
-    const int me = (int)ln.size();
-    ln.emplace_back();
-    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    double cmn[3] = {INFINITY, INFINITY, INFINITY}, cmx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int i = lo; i < hi; i++) {
-        double a[3], b[3];
-        tri_bounds(tris + (size_t)PTMI_TRIANGLE_BYTES * idx[i], a, b);
-        for (int k = 0; k < 3; k++) {
-            mn[k] = std::min(mn[k], a[k]);
-            mx[k] = std::max(mx[k], b[k]);
-            const double c = 0.5 * (a[k] + b[k]);
-            cmn[k] = std::min(cmn[k], c);
-            cmx[k] = std::max(cmx[k], c);
-        }
-    }
-    // Conservative expansion: far beyond the rounding error of a computed hit point.
-    double scale = 0.0;
-    for (int k = 0; k < 3; k++) scale = std::max({scale, std::fabs(mn[k]), std::fabs(mx[k]), mx[k] - mn[k]});
-    const double m = 1e-7 * scale + 1e-300;
-    LocalNode L{};
-    for (int k = 0; k < 3; k++) {
-        L.bb_min[k] = mn[k] - m;
-        L.bb_max[k] = mx[k] + m;
-    }
-    if (hi - lo <= 4) {
-        L.left = L.right = -1;
-        L.first = (int32_t)ht.size();
-        L.count = hi - lo;
-        std::sort(idx.begin() + lo, idx.begin() + hi);
-        for (int i = lo; i < hi; i++) {
-            const uint8_t* b = tris + (size_t)PTMI_TRIANGLE_BYTES * idx[i];
-            DevTri t{};
-            std::memcpy(t.p1, b + 0, 24);
-            std::memcpy(t.e1, b + 96, 24);
-            std::memcpy(t.e2, b + 128, 24);
-            t.n = idx[i];
-            ht.push_back(t);
-        }
-    } else {
-        int ax = 0;
-        for (int k = 1; k < 3; k++)
-            if (cmx[k] - cmn[k] > cmx[ax] - cmn[ax]) ax = k;
-        const int mid = (lo + hi) / 2;
-        std::nth_element(idx.begin() + lo, idx.begin() + mid, idx.begin() + hi, [&](int32_t a, int32_t b) {
-            double amn[3], amx[3], bmn[3], bmx[3];
-            tri_bounds(tris + (size_t)PTMI_TRIANGLE_BYTES * a, amn, amx);
-            tri_bounds(tris + (size_t)PTMI_TRIANGLE_BYTES * b, bmn, bmx);
-            const double ca = amn[ax] + amx[ax], cb = bmn[ax] + bmx[ax];
-            return ca < cb || (ca == cb && a < b);
-        });
-        L.first = L.count = 0;
-        L.left = build_local_rec(tris, idx, lo, mid, ln, ht);
-        L.right = build_local_rec(tris, idx, mid, hi, ln, ht);
-    }
-    ln[me] = L;
-    return me;
-}
-
-int build_local_bvh(const uint8_t* tris, int32_t off, int32_t cnt, std::vector<LocalNode>& ln,
-                    std::vector<DevTri>& ht) {
-    std::vector<int32_t> idx(cnt);
-    for (int32_t i = 0; i < cnt; i++) idx[i] = off + i;
-    return build_local_rec(tris, idx, 0, cnt, ln, ht);
-}
-
 int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, uint32_t n_tri, const uint8_t* groups,
                   uint32_t n_grp, const uint8_t* camera, std::vector<DevObject>& objs, std::vector<int32_t>& roots,
-                  std::vector<DevNode>& nodes, std::vector<LocalNode>& lnodes, std::vector<DevTri>& ht,
+                  std::vector<DevNode>& nodes, RootIndex& index, std::vector<RootRec>& root_rec,
                   std::vector<DevTriShade>& st, DevCamera& cam, int32_t run_end[5], char* err, size_t err_len) {
     if (!objects || n_obj == 0 || n_obj > PTMI_MAX_OBJECTS) {
         set_err(err, err_len, "need 1..%d objects (tracer.cl:846 __local object objects[16]), got %u",
@@ -290,7 +204,6 @@ int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, u
         tri_cnt[g] = rd<int32_t>(b + 132);
         n.child0 = rd<int32_t>(b + 140);
         n.child1 = rd<int32_t>(b + 144);
-        n.local = -1;
         if (tri_cnt[g] < 0 || tri_off[g] < 0 || (int64_t)tri_off[g] + tri_cnt[g] > (int64_t)n_tri ||
             n.child0 >= (int32_t)n_grp || n.child1 >= (int32_t)n_grp) {
             set_err(err, err_len, "group %u: triangle range [%d,+%d) / children (%d,%d) out of range", g,
@@ -298,25 +211,13 @@ int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, u
             return PTMI_ERR_ARG;
         }
     }
-    // BVH depth: the kernel's per-lane LDS stack (kStack = 48 entries) holds one
-    // pending sibling per reference level, plus 3 pushes at a node, plus one
-    // pending sibling per level of that node's triangle sub-BVH.
-    int maxd = 0;
-    {
-        std::vector<int> depth(n_grp, 0);
-        for (int32_t g = (int32_t)n_grp - 1; g >= 0; g--) {  // children have larger (preorder) indices
-            int dd = 0;
-            if (nodes[g].child0 > 0) dd = std::max(dd, depth[nodes[g].child0] + 1);
-            if (nodes[g].child1 > 0) dd = std::max(dd, depth[nodes[g].child1] + 1);
-            depth[g] = dd;
-            maxd = std::max(maxd, dd);
+    // Children must follow their parent (BuildCLGroup preorder numbering): the
+    // trees are then acyclic and every walk terminates.
+    for (int32_t g = 0; g < (int32_t)n_grp; g++)
+        if ((nodes[g].child0 > 0 && nodes[g].child0 <= g) || (nodes[g].child1 > 0 && nodes[g].child1 <= g)) {
+            set_err(err, err_len, "group %d: child index not in preorder (BuildCLGroup numbering)", g);
+            return PTMI_ERR_ARG;
         }
-        for (int32_t g = 0; g < (int32_t)n_grp; g++)
-            if ((nodes[g].child0 > 0 && nodes[g].child0 <= g) || (nodes[g].child1 > 0 && nodes[g].child1 <= g)) {
-                set_err(err, err_len, "group %d: child index not in preorder (BuildCLGroup numbering)", g);
-                return PTMI_ERR_ARG;
-            }
-    }
     st.resize(n_tri);
     for (uint32_t t = 0; t < n_tri; t++) {
         const uint8_t* b = tris + (size_t)PTMI_TRIANGLE_BYTES * t;
@@ -325,22 +226,19 @@ int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, u
         std::memcpy(st[t].n3, b + 224, 32);
         std::memcpy(st[t].color, b + 256, 32);
     }
-    // Per reference node: a sub-BVH over its triangle list (median splits on the
-    // largest centroid extent, leaves <= 4 triangles).  Triangle records are
-    // stored in leaf order; each keeps its reference index.
-    ht.clear();
-    lnodes.clear();
-    for (uint32_t g = 0; g < n_grp; g++)
-        if (tri_cnt[g] > 0) nodes[g].local = build_local_bvh(tris, tri_off[g], tri_cnt[g], lnodes, ht);
-    std::vector<int> ldepth(lnodes.size(), 0);
-    int maxl = 0;
-    for (int32_t i = (int32_t)lnodes.size() - 1; i >= 0; i--) {  // children follow their parent
-        if (lnodes[i].left >= 0) ldepth[i] = 1 + std::max(ldepth[lnodes[i].left], ldepth[lnodes[i].right]);
-        maxl = std::max(maxl, ldepth[i]);
-    }
-    if (maxd + maxl + 4 > 48) {
-        set_err(err, err_len, "BVH depth %d (+ %d triangle sub-tree levels) exceeds the traversal stack", maxd, maxl);
-        return PTMI_ERR_UNSUPPORTED;
+    // Per distinct BVH root: the triangle traversal index (ptmi_bvh.cpp).
+    index = RootIndex{};
+    root_rec.assign(roots.size(), RootRec{});
+    std::vector<int32_t> built(n_grp, -1);  // roots shared by several objects are built once
+    for (size_t i = 0; i < roots.size(); i++) {
+        const int32_t r = roots[i];
+        if (built[r] < 0) {
+            const int rc = build_root_index(tris, nodes, tri_off, tri_cnt, r, index, &root_rec[i], err, err_len);
+            if (rc) return rc;
+            built[r] = (int32_t)i;
+        } else {
+            root_rec[i] = root_rec[built[r]];
+        }
     }
     return PTMI_OK;
 }
@@ -388,13 +286,13 @@ int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, con
     std::vector<DevObject> objs;
     std::vector<int32_t> roots;
     std::vector<DevNode> nodes;
-    std::vector<LocalNode> lnodes;
-    std::vector<DevTri> ht;
+    RootIndex index;
+    std::vector<RootRec> root_rec;
     std::vector<DevTriShade> st;
     DevCamera cam{};
     int32_t run_end[5];
     rc = convert_scene((const uint8_t*)objects, n_obj, (const uint8_t*)triangles, n_tri, (const uint8_t*)groups, n_grp,
-                       (const uint8_t*)camera, objs, roots, nodes, lnodes, ht, st, cam, run_end, err, err_len);
+                       (const uint8_t*)camera, objs, roots, nodes, index, root_rec, st, cam, run_end, err, err_len);
     if (rc) return rc;
     int flags = 0;
     for (const DevObject& o : objs) {
@@ -411,8 +309,10 @@ int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, con
     s->width = (uint32_t)cam.width;
     s->height = (uint32_t)cam.height;
     if ((rc = upload(objs, &s->buffers[0], err, err_len)) || (rc = upload(roots, &s->buffers[1], err, err_len)) ||
-        (rc = upload(nodes, &s->buffers[2], err, err_len)) || (rc = upload(ht, &s->buffers[3], err, err_len)) ||
-        (rc = upload(st, &s->buffers[4], err, err_len)) || (rc = upload(lnodes, &s->buffers[7], err, err_len))) {
+        (rc = upload(nodes, &s->buffers[2], err, err_len)) || (rc = upload(index.tris, &s->buffers[3], err, err_len)) ||
+        (rc = upload(st, &s->buffers[4], err, err_len)) || (rc = upload(index.nodes, &s->buffers[7], err, err_len)) ||
+        (rc = upload(index.chain_boxes, &s->buffers[8], err, err_len)) ||
+        (rc = upload(root_rec, &s->buffers[9], err, err_len))) {
         ptmi_scene_destroy(s);
         return rc;
     }
@@ -460,7 +360,9 @@ int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, con
     s->dev.nodes = (const DevNode*)s->buffers[2];
     s->dev.tris = (const DevTri*)s->buffers[3];
     s->dev.tri_shade = (const DevTriShade*)s->buffers[4];
-    s->dev.lnodes = (const LocalNode*)s->buffers[7];
+    s->dev.nodes4 = (const Node4*)s->buffers[7];
+    s->dev.chains = (const ChainBox*)s->buffers[8];
+    s->dev.root_rec = (const RootRec*)s->buffers[9];
     s->dev.n_obj = (uint32_t)objs.size();
     s->dev.n_list = n_obj;
     s->dev.n_nodes = n_grp;

@@ -1,0 +1,335 @@
+// ptmi_bvh.cpp -- traversal structure for the triangles of one reference BVH root.
+//
+// The reference walks its own BVH (CLGroup preorder array, tracer.cl:617-719):
+// a triangle of node g is a candidate of a ray iff the ray's LINE passes the
+// reference box test (intersectRayWithBox, tracer.cl:270-280) of every node on
+// the path root -> g.  That tree keeps 46 % of the teapot's triangles on inner
+// nodes (up to 305 per node, bvh.go:92-119), so walking it costs hundreds of
+// triangle tests per ray.
+//
+// Here each root's triangles get a second, independent index: a 4-wide SAH BVH
+// with conservatively widened boxes.  The kernel uses it to FIND the triangles
+// a ray hits, then admits a hit as a candidate only after checking the
+// reference gate above for that triangle (its "chain": the boxes of the
+// reference nodes strictly below the root down to g, tested with the
+// reference's exact arithmetic).  Candidate set and tie-break order are the
+// reference's, so the winner is too; see DESIGN.md "Parity contract".
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/ptmi.h"
+#include "ptmi_bvh.h"
+
+namespace ptmi {
+namespace {
+
+template <typename T>
+T rd(const uint8_t* p) {
+    T v;
+    std::memcpy(&v, p, sizeof(T));
+    return v;
+}
+
+struct Prim {
+    double mn[3], mx[3], c[3];
+    int32_t tri;    // reference triangle index
+    int32_t chain;  // (chain offset << 5) | chain length
+};
+
+struct BNode {  // binary build node
+    double mn[3], mx[3];
+    int left = -1, right = -1;  // inner: children; leaf: left = -1
+    int first = 0, count = 0;   // leaf: prims [first, first + count)
+};
+
+constexpr int kLeafMax = 7;         // 3-bit count in the leaf entry code
+constexpr int kMaxBinaryDepth = 14; // BVH4 depth <= 7: 3 pushes per level fit kStack = 24
+constexpr int kBins = 32;
+
+double area(const double* mn, const double* mx) {
+    const double dx = mx[0] - mn[0], dy = mx[1] - mn[1], dz = mx[2] - mn[2];
+    return (dx < 0 || dy < 0 || dz < 0) ? 0.0 : 2.0 * (dx * dy + dy * dz + dz * dx);
+}
+
+void grow(double* mn, double* mx, const double* a, const double* b) {
+    for (int k = 0; k < 3; k++) {
+        mn[k] = std::min(mn[k], a[k]);
+        mx[k] = std::max(mx[k], b[k]);
+    }
+}
+
+struct Builder {
+    std::vector<Prim>& prims;
+    std::vector<BNode> nodes;
+    explicit Builder(std::vector<Prim>& p) : prims(p) {}
+
+    int make_leaf(int lo, int hi, const double* mn, const double* mx) {
+        BNode n;
+        std::memcpy(n.mn, mn, 24);
+        std::memcpy(n.mx, mx, 24);
+        n.first = lo;
+        n.count = hi - lo;
+        nodes.push_back(n);
+        return (int)nodes.size() - 1;
+    }
+
+    int build(int lo, int hi, int depth) {
+        double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+        double cmn[3] = {INFINITY, INFINITY, INFINITY}, cmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = lo; i < hi; i++) {
+            grow(mn, mx, prims[i].mn, prims[i].mx);
+            grow(cmn, cmx, prims[i].c, prims[i].c);
+        }
+        const int n = hi - lo;
+        if (n <= 2) return make_leaf(lo, hi, mn, mx);
+        // Depth budget: when the remaining levels barely suffice for a balanced
+        // tree, split at the median (guarantees depth <= kMaxBinaryDepth).
+        int need = 0;
+        while ((kLeafMax << need) < n) need++;
+        int axis = 0;
+        for (int k = 1; k < 3; k++)
+            if (cmx[k] - cmn[k] > cmx[axis] - cmn[axis]) axis = k;
+        int mid = -1;
+        if (need + 1 >= kMaxBinaryDepth - depth || cmx[axis] - cmn[axis] <= 0.0) {
+            if (n <= kLeafMax) return make_leaf(lo, hi, mn, mx);
+            mid = (lo + hi) / 2;
+            std::nth_element(prims.begin() + lo, prims.begin() + mid, prims.begin() + hi,
+                             [axis](const Prim& a, const Prim& b) {
+                                 return a.c[axis] < b.c[axis] || (a.c[axis] == b.c[axis] && a.tri < b.tri);
+                             });
+        } else {
+            // Binned SAH over all three axes.
+            double best = INFINITY;
+            int best_axis = -1, best_bin = -1;
+            for (int k = 0; k < 3; k++) {
+                const double ext = cmx[k] - cmn[k];
+                if (ext <= 0.0) continue;
+                double bmn[kBins][3], bmx[kBins][3];
+                int bc[kBins] = {0};
+                for (int b = 0; b < kBins; b++)
+                    for (int q = 0; q < 3; q++) bmn[b][q] = INFINITY, bmx[b][q] = -INFINITY;
+                const double s = kBins / ext;
+                for (int i = lo; i < hi; i++) {
+                    int b = std::min(kBins - 1, (int)((prims[i].c[k] - cmn[k]) * s));
+                    bc[b]++;
+                    grow(bmn[b], bmx[b], prims[i].mn, prims[i].mx);
+                }
+                double rmn[3] = {INFINITY, INFINITY, INFINITY}, rmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+                double ra[kBins];
+                int rc[kBins];
+                int cnt = 0;
+                for (int b = kBins - 1; b > 0; b--) {
+                    grow(rmn, rmx, bmn[b], bmx[b]);
+                    cnt += bc[b];
+                    ra[b] = area(rmn, rmx) * cnt;
+                    rc[b] = cnt;
+                }
+                double lmn[3] = {INFINITY, INFINITY, INFINITY}, lmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+                cnt = 0;
+                for (int b = 0; b < kBins - 1; b++) {
+                    grow(lmn, lmx, bmn[b], bmx[b]);
+                    cnt += bc[b];
+                    if (cnt == 0 || rc[b + 1] == 0) continue;
+                    const double cost = area(lmn, lmx) * cnt + ra[b + 1];
+                    if (cost < best) {
+                        best = cost;
+                        best_axis = k;
+                        best_bin = b;
+                    }
+                }
+            }
+            const double leaf_cost = area(mn, mx) * n;
+            if (n <= kLeafMax && (best_axis < 0 || leaf_cost <= 1.2 * best + area(mn, mx)))
+                return make_leaf(lo, hi, mn, mx);
+            if (best_axis < 0) {
+                mid = (lo + hi) / 2;
+                std::nth_element(prims.begin() + lo, prims.begin() + mid, prims.begin() + hi,
+                                 [axis](const Prim& a, const Prim& b) {
+                                     return a.c[axis] < b.c[axis] || (a.c[axis] == b.c[axis] && a.tri < b.tri);
+                                 });
+            } else {
+                const double s = kBins / (cmx[best_axis] - cmn[best_axis]);
+                const double c0 = cmn[best_axis];
+                auto it = std::partition(prims.begin() + lo, prims.begin() + hi, [&](const Prim& p) {
+                    return std::min(kBins - 1, (int)((p.c[best_axis] - c0) * s)) <= best_bin;
+                });
+                mid = (int)(it - prims.begin());
+                if (mid == lo || mid == hi) mid = (lo + hi) / 2;
+            }
+        }
+        const int me = (int)nodes.size();
+        nodes.emplace_back();
+        const int l = build(lo, mid, depth + 1);
+        const int r = build(mid, hi, depth + 1);
+        BNode& nd = nodes[me];
+        std::memcpy(nd.mn, mn, 24);
+        std::memcpy(nd.mx, mx, 24);
+        nd.left = l;
+        nd.right = r;
+        return me;
+    }
+};
+
+// Leaf entry code shared by Node4::child and the kernel's traversal stack
+// (count 0 never occurs: leaves hold 1..kLeafMax triangles).
+int32_t leaf_code(int32_t first, int32_t count) { return -((first << 3) | count) - 1; }
+
+}  // namespace
+
+int build_root_index(const uint8_t* tris, const std::vector<DevNode>& nodes, const std::vector<int32_t>& tri_off,
+                     const std::vector<int32_t>& tri_cnt, int32_t root, RootIndex& out, RootRec* rec, char* err,
+                     size_t err_len) {
+    *rec = RootRec{};
+    int32_t* entry = &rec->entry;
+    // Reference subtree of `root` (children > 0 are present, tracer.cl:683/704)
+    // with each node's gate chain relative to the root.
+    std::vector<Prim> prims;
+    std::vector<std::pair<int32_t, std::vector<int32_t>>> todo{{root, {root}}};
+    while (!todo.empty()) {
+        auto [g, path] = todo.back();
+        todo.pop_back();
+        if (path.size() > 31) {
+            std::snprintf(err, err_len, "reference BVH deeper than 30 levels below root %d", root);
+            return PTMI_ERR_UNSUPPORTED;
+        }
+        const int32_t off = (int32_t)out.chain_boxes.size();
+        for (int32_t k : path) {
+            ChainBox b;
+            std::memcpy(b.mn, nodes[k].bb_min, 24);
+            std::memcpy(b.mx, nodes[k].bb_max, 24);
+            out.chain_boxes.push_back(b);
+        }
+        const int32_t chain = (off << 5) | (int32_t)path.size();
+        for (int32_t t = tri_off[g]; t < tri_off[g] + tri_cnt[g]; t++) {
+            const uint8_t* b = tris + (size_t)PTMI_TRIANGLE_BYTES * t;
+            Prim p;
+            double v[5][3];
+            for (int k = 0; k < 3; k++) {
+                v[0][k] = rd<double>(b + 0 + 8 * k);
+                v[1][k] = rd<double>(b + 32 + 8 * k);
+                v[2][k] = rd<double>(b + 64 + 8 * k);
+                v[3][k] = v[0][k] + rd<double>(b + 96 + 8 * k);   // the p1 + e1, p1 + e2 that
+                v[4][k] = v[0][k] + rd<double>(b + 128 + 8 * k);  // Moller-Trumbore spans
+            }
+            for (int k = 0; k < 3; k++) {
+                p.mn[k] = p.mx[k] = v[0][k];
+                for (int i = 1; i < 5; i++) {
+                    p.mn[k] = std::min(p.mn[k], v[i][k]);
+                    p.mx[k] = std::max(p.mx[k], v[i][k]);
+                }
+                p.c[k] = 0.5 * (p.mn[k] + p.mx[k]);
+            }
+            p.tri = t;
+            p.chain = chain;
+            prims.push_back(p);
+        }
+        for (int32_t c : {nodes[g].child1, nodes[g].child0})
+            if (c > 0) {
+                auto q = path;
+                q.push_back(c);
+                todo.push_back({c, q});
+            }
+    }
+    if (prims.empty()) {  // nothing to intersect: an empty hull no slab test passes
+        *entry = kEmptyChild;
+        for (int k = 0; k < 3; k++) rec->hull_mn[k] = 1.0, rec->hull_mx[k] = -1.0;
+        return PTMI_OK;
+    }
+    if (prims.size() > ((size_t)kLeafMax << kMaxBinaryDepth)) {
+        std::snprintf(err, err_len, "BVH root %d holds %zu triangles (max %d per root)", root, prims.size(),
+                      kLeafMax << kMaxBinaryDepth);
+        return PTMI_ERR_UNSUPPORTED;
+    }
+    // Non-finite vertices would void the conservative box argument.
+    for (const Prim& p : prims)
+        for (int k = 0; k < 3; k++)
+            if (!std::isfinite(p.mn[k]) || !std::isfinite(p.mx[k])) {
+                std::snprintf(err, err_len, "triangle %d has non-finite vertices", p.tri);
+                return PTMI_ERR_UNSUPPORTED;
+            }
+    Builder B(prims);
+    const int broot = B.build(0, (int)prims.size(), 0);
+
+    // Conservative widening: far beyond the ~1e-15 relative error of a computed
+    // Moller-Trumbore hit point and of the slab arithmetic in the kernel.
+    double scale = 0.0;
+    for (const Prim& p : prims)
+        for (int k = 0; k < 3; k++) scale = std::max({scale, std::fabs(p.mn[k]), std::fabs(p.mx[k])});
+    const double m = 1e-7 * scale + 1e-300;
+    for (int k = 0; k < 3; k++) {
+        rec->hull_mn[k] = B.nodes[broot].mn[k] - m;
+        rec->hull_mx[k] = B.nodes[broot].mx[k] + m;
+    }
+
+    // Triangles in leaf order.
+    const int32_t tri_base = (int32_t)out.tris.size();
+    std::vector<int32_t> leaf_first(B.nodes.size(), 0);
+    for (size_t i = 0; i < B.nodes.size(); i++) {
+        const BNode& n = B.nodes[i];
+        if (n.left >= 0) continue;
+        leaf_first[i] = (int32_t)out.tris.size();
+        std::vector<Prim> lp(prims.begin() + n.first, prims.begin() + n.first + n.count);
+        std::sort(lp.begin(), lp.end(), [](const Prim& a, const Prim& b) { return a.tri < b.tri; });
+        for (const Prim& p : lp) {
+            const uint8_t* b = tris + (size_t)PTMI_TRIANGLE_BYTES * p.tri;
+            DevTri t{};
+            std::memcpy(t.p1, b + 0, 24);
+            std::memcpy(t.e1, b + 96, 24);
+            std::memcpy(t.e2, b + 128, 24);
+            t.n = p.tri;
+            t.chain = p.chain;
+            out.tris.push_back(t);
+        }
+    }
+    (void)tri_base;
+    auto code_of = [&](int bi) -> int32_t {
+        const BNode& n = B.nodes[bi];
+        return n.left < 0 ? leaf_code(leaf_first[bi], n.count) : -2;  // -2: inner, resolved below
+    };
+    // Collapse the binary tree to 4-wide nodes (children = grandchildren of
+    // inner children), emitted in creation order.
+    std::vector<std::pair<int, int>> work;  // (binary node, Node4 slot)
+    auto emit = [&](int bi) -> int32_t {
+        if (B.nodes[bi].left < 0) return code_of(bi);
+        const int32_t slot = (int32_t)out.nodes.size();
+        out.nodes.emplace_back();
+        work.push_back({bi, slot});
+        return slot;
+    };
+    *entry = emit(broot);
+    while (!work.empty()) {
+        auto [bi, slot] = work.back();
+        work.pop_back();
+        int kids[4], nk = 0;
+        for (int c : {B.nodes[bi].left, B.nodes[bi].right}) {
+            if (B.nodes[c].left >= 0) {
+                kids[nk++] = B.nodes[c].left;
+                kids[nk++] = B.nodes[c].right;
+            } else {
+                kids[nk++] = c;
+            }
+        }
+        Node4 nd{};
+        for (int i = 0; i < 4; i++) {
+            if (i < nk) {
+                const BNode& c = B.nodes[kids[i]];
+                for (int k = 0; k < 3; k++) {
+                    nd.mn[k][i] = c.mn[k] - m;
+                    nd.mx[k][i] = c.mx[k] + m;
+                }
+                nd.child[i] = 0;  // patched after emit (emit may grow out.nodes)
+            } else {
+                for (int k = 0; k < 3; k++) nd.mn[k][i] = nd.mx[k][i] = 0.0;
+                nd.child[i] = kEmptyChild;
+            }
+        }
+        for (int i = 0; i < nk; i++) nd.child[i] = emit(kids[i]);
+        out.nodes[slot] = nd;
+    }
+    return PTMI_OK;
+}
+
+}  // namespace ptmi

@@ -14,6 +14,7 @@
 // reads it, so results are bit-faithful (see DESIGN.md "Parity contract").
 #pragma once
 #include <stdint.h>
+#include <limits.h>
 
 namespace ptmi {
 
@@ -37,37 +38,52 @@ struct alignas(16) DevObject {
     int32_t pad[2];
 };
 
-// Reference BVH node (CLGroup, tracer.cl:24-35).  Its exact line-box test is
-// the gate that decides which triangles are candidates, as in the reference.
+// Reference BVH node (CLGroup, tracer.cl:24-35): its box gates the triangles
+// below it (the kernel tests it with the reference's exact line-box decision).
 struct alignas(16) DevNode {
     double bb_min[3];
     double bb_max[3];
     int32_t child0, child1;  // > 0 means present (tracer.cl:683, 704)
-    int32_t local;           // root of this node's triangle sub-BVH (LocalNode index), -1: no triangles
-    int32_t pad;
+    int32_t pad[2];
 };
 static_assert(sizeof(DevNode) == 64, "DevNode must stay 64 B");
 
-// Sub-BVH over ONE reference node's triangle list (built on the host): boxes are
-// the triangles' bounds expanded by a conservative margin, so a ray that misses
-// a LocalNode box cannot produce a Moller-Trumbore hit inside it.
-struct alignas(16) LocalNode {
-    double bb_min[3];
-    double bb_max[3];
-    int32_t left, right;     // children (LocalNode indices), left < 0: leaf
-    int32_t first, count;    // leaf: triangles [first, first + count) of DevScene::tris
-};
-static_assert(sizeof(LocalNode) == 64, "LocalNode must stay 64 B");
-
-// Triangle in sub-BVH leaf order; `n` is its index in the reference's triangle
-// list (tie-break order and DevTriShade slot).
+// Triangle in traversal-index leaf order; `n` is its index in the reference's
+// triangle list (tie-break order and DevTriShade slot), `chain` locates its gate
+// chain: ChainBox[chain >> 5 .. + (chain & 31)) (see ptmi_bvh.cpp).
 struct alignas(16) DevTri {
     double p1[3];
     double e1[3];
     double e2[3];
-    int32_t n, pad;
+    int32_t n, chain;
 };
 static_assert(sizeof(DevTri) == 80, "DevTri must stay 80 B");
+
+// Box of a reference node on a triangle's gate chain.
+struct alignas(16) ChainBox {
+    double mn[3], mx[3];
+};
+
+// 4-wide traversal node over one reference root's triangles (ptmi_bvh.cpp).
+// Boxes are widened conservatively; child[i] is a Node4 index (>= 0), a leaf
+// code -((first << 3) | count) - 1 (triangles [first, first + count) of
+// DevScene::tris), or kEmptyChild.
+struct alignas(16) Node4 {
+    double mn[3][4];  // [axis][child]
+    double mx[3][4];
+    int32_t child[4];
+};
+static_assert(sizeof(Node4) == 208, "Node4 must stay 208 B");
+constexpr int32_t kEmptyChild = INT32_MIN;
+
+// One BVH root of a group object: the widened hull of all its triangles (the
+// cull test before its walk) and the entry code of its Node4 index.
+struct alignas(16) RootRec {
+    double hull_mn[3], hull_mx[3];
+    int32_t entry;
+    int32_t pad;
+};
+static_assert(sizeof(RootRec) == 64, "RootRec must stay 64 B");
 
 struct alignas(16) DevTriShade {
     double n1[4], n2[4], n3[4];
@@ -105,8 +121,10 @@ struct DevScene {
     int32_t n_spheres_st;
     int32_t pad1;
     const int32_t* roots;  // concatenated group roots of all type-4 objects
+    const RootRec* root_rec;  // per roots[] slot
     const DevNode* nodes;
-    const LocalNode* lnodes;
+    const Node4* nodes4;
+    const ChainBox* chains;
     const DevTri* tris;
     const DevTriShade* tri_shade;
     uint32_t n_obj;   // intersectable objects in objs[]

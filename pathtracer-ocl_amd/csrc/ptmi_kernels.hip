@@ -243,7 +243,10 @@ __device__ __forceinline__ bool ray_box_ref(d4 o, d4 d, d4 r, const double* mn, 
 
 // Moller-Trumbore (tracer.cl:640-675) on the 3 live components: the w terms of
 // the reference's dot() products multiply a cross() result whose w is exactly 0.
-__device__ __forceinline__ void tri_test(const DevTri& T, d4 o, d4 d, int slot, int key, Hit& h) {
+__device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o, d4 d, d4 r);
+
+__device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 o, d4 d, d4 r, int slot, int key,
+                                         Hit& h, int& vchain) {
     const double e1x = T.e1[0], e1y = T.e1[1], e1z = T.e1[2];
     const double e2x = T.e2[0], e2y = T.e2[1], e2z = T.e2[2];
     // dirCrossE2 = cross(d, e2)
@@ -276,6 +279,13 @@ __device__ __forceinline__ void tri_test(const DevTri& T, d4 o, d4 d, int slot, 
     const double t = f * dt;
     const int n = T.n;
     if (better_tri(h, t, key, n)) {
+        // Admit the hit only if the reference would have tested this triangle:
+        // its gate chain (root -> its node) passes the exact line-box tests.
+        const int c = T.chain;
+        if (c != vchain) {
+            if (!verify_chain(S, c, o, d, r)) return;
+            vchain = c;
+        }
         h.t = t;
         h.obj = slot;
         h.key = key;
@@ -285,74 +295,83 @@ __device__ __forceinline__ void tri_test(const DevTri& T, d4 o, d4 d, int slot, 
     }
 }
 
-static constexpr int kStack = 48;  // per-lane LDS traversal stack (host checks the bound)
+static constexpr int kStack = 24;  // per-lane LDS traversal stack (3 pushes x BVH4 depth <= 7, ptmi_bvh.cpp)
 
-// Stack entries: >= 0 a reference node, <= -2 the sub-BVH node -(e + 2).
-__device__ __forceinline__ int enc_local(int i) { return -(i + 2); }
+// The reference's gate for one triangle: every reference node on the path from
+// the walked root to the triangle's node passes intersectRayWithBox
+// (tracer.cl:617-719).  Boxes are contiguous, so their loads are independent.
+__device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o, d4 d, d4 r) {
+    const ChainBox* B = S.chains + (chain >> 5);
+    const int len = chain & 31;
+    for (int i = 0; i < len; i++) {
+        double a, b;
+        if (!ray_box_ref(o, d, r, B[i].mn, B[i].mx, a, b)) return false;
+    }
+    return true;
+}
 
-// BVH walk of one group root.
-//  * Reference nodes gate exactly as in the reference (same line-box decision,
-//    ray_box_ref), so the set of candidate triangles is the reference's; nodes
-//    whose box cannot hold a winning t are skipped (prune_margin).
-//  * A passed node's own triangles are reached through its sub-BVH, whose boxes
-//    are the triangles' bounds widened by 1e-7 x scene scale: a ray that misses
-//    such a box by the slab test below cannot yield a Moller-Trumbore hit inside
-//    it (the computed hit point is within ~1e-15 relative of the triangle).
-//  * Ties resolve through better_tri (triangle index), so the winner is the
-//    reference's whatever the visiting order.
-__device__ __forceinline__ void walk_group(const DevScene& S, int* __restrict__ stk, int root, int slot, int key,
-                                           d4 o, d4 d, d4 r, Hit& h) {
+// Conservative slab test against a widened traversal box: false only when no
+// t in [kEps, h.t] (with margins) can lie in the box.  A NaN bound (NaN ray)
+// fails every comparison, so the box is entered.
+__device__ __forceinline__ bool cull_box(d4 o, d4 r, double mnx, double mny, double mnz, double mxx, double mxy,
+                                         double mxz, double lim, double& tn) {
+    const double ax = (mnx - o.x) * r.x, bx = (mxx - o.x) * r.x;
+    const double ay = (mny - o.y) * r.y, by = (mxy - o.y) * r.y;
+    const double az = (mnz - o.z) * r.z, bz = (mxz - o.z) * r.z;
+    tn = max3(fmin(ax, bx), fmin(ay, by), fmin(az, bz));
+    const double tf = min3(fmax(ax, bx), fmax(ay, by), fmax(az, bz));
+    return tn > tf || tn > lim || tf + prune_margin(tf) < kEps;
+}
+
+// Closest-hit walk of one root's 4-wide traversal index (ptmi_bvh.cpp): nearest
+// child first, the others pushed far-to-near.  Which triangles are FOUND does
+// not depend on the visiting order or the widened boxes (every triangle that
+// can produce a winning t is reached); ties resolve through better_tri.
+__device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, int entry, int slot, int key,
+                                           d4 o, d4 d, d4 r, Hit& h, int& vchain) {
     int sp = 0;
-    stk[(sp++) * 256] = root;
-    while (sp > 0) {
-        const int e = stk[(--sp) * 256];
-        if (e >= 0) {
-            const DevNode& N = S.nodes[e];
-            double tlo, thi;
-            if (!ray_box_ref(o, d, r, N.bb_min, N.bb_max, tlo, thi)) continue;
-            if (tlo > h.t + prune_margin(h.t) || thi + prune_margin(thi) < kEps) continue;
-            const int c0 = N.child0, c1 = N.child1;
-            if (c0 > 0 && c1 > 0) {
-                // near child visited first: order by box centre along the ray
-                const DevNode& A = S.nodes[c0];
-                const DevNode& B = S.nodes[c1];
-                const double ka = (A.bb_min[0] + A.bb_max[0]) * d.x + (A.bb_min[1] + A.bb_max[1]) * d.y +
-                                  (A.bb_min[2] + A.bb_max[2]) * d.z;
-                const double kb = (B.bb_min[0] + B.bb_max[0]) * d.x + (B.bb_min[1] + B.bb_max[1]) * d.y +
-                                  (B.bb_min[2] + B.bb_max[2]) * d.z;
-                const bool a_first = ka <= kb;
-                stk[(sp++) * 256] = a_first ? c1 : c0;
-                stk[(sp++) * 256] = a_first ? c0 : c1;
-            } else if (c0 > 0) {
-                stk[(sp++) * 256] = c0;
-            } else if (c1 > 0) {
-                stk[(sp++) * 256] = c1;
+    int cur = entry;
+    while (true) {
+        if (cur >= 0) {
+            const Node4& N = S.nodes4[cur];
+            const double lim = h.t + prune_margin(h.t);
+            double k[4];
+            int c[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                double tn;
+                c[i] = N.child[i];
+                const bool cull = cull_box(o, r, N.mn[0][i], N.mn[1][i], N.mn[2][i], N.mx[0][i], N.mx[1][i],
+                                           N.mx[2][i], lim, tn) ||
+                                  c[i] == kEmptyChild;
+                k[i] = cull ? __builtin_huge_val() : fmax(tn, -__builtin_huge_val());  // NaN -> -inf
             }
-            if (N.local >= 0) stk[(sp++) * 256] = enc_local(N.local);  // own triangles first
-        } else {
-            const LocalNode& L = S.lnodes[-e - 2];
-            const double ax = (L.bb_min[0] - o.x) * r.x, bx = (L.bb_max[0] - o.x) * r.x;
-            const double ay = (L.bb_min[1] - o.y) * r.y, by = (L.bb_max[1] - o.y) * r.y;
-            const double az = (L.bb_min[2] - o.z) * r.z, bz = (L.bb_max[2] - o.z) * r.z;
-            const double tn = max3(fmin(ax, bx), fmin(ay, by), fmin(az, bz));
-            const double tf = min3(fmax(ax, bx), fmax(ay, by), fmax(az, bz));
-            // (NaN bounds -- a NaN ray -- fail every test below: the node is visited.)
-            if (tn > tf || tn > h.t + prune_margin(h.t) || tf + prune_margin(tf) < kEps) continue;
-            if (L.left < 0) {
-                const int end = L.first + L.count;
-                for (int i = L.first; i < end; i++) tri_test(S.tris[i], o, d, slot, key, h);
-            } else {
-                const LocalNode& A = S.lnodes[L.left];
-                const LocalNode& B = S.lnodes[L.right];
-                const double ka = (A.bb_min[0] + A.bb_max[0]) * d.x + (A.bb_min[1] + A.bb_max[1]) * d.y +
-                                  (A.bb_min[2] + A.bb_max[2]) * d.z;
-                const double kb = (B.bb_min[0] + B.bb_max[0]) * d.x + (B.bb_min[1] + B.bb_max[1]) * d.y +
-                                  (B.bb_min[2] + B.bb_max[2]) * d.z;
-                const bool a_first = ka <= kb;
-                stk[(sp++) * 256] = enc_local(a_first ? L.right : L.left);
-                stk[(sp++) * 256] = enc_local(a_first ? L.left : L.right);
+            // sort (k, c) ascending: 5 compare-exchanges
+#define PTMI_CX(a, b)                                      \
+    if (k[b] < k[a]) {                                     \
+        const double tk = k[a];                            \
+        k[a] = k[b];                                       \
+        k[b] = tk;                                         \
+        const int tc = c[a];                               \
+        c[a] = c[b];                                       \
+        c[b] = tc;                                         \
+    }
+            PTMI_CX(0, 1) PTMI_CX(2, 3) PTMI_CX(0, 2) PTMI_CX(1, 3) PTMI_CX(1, 2)
+#undef PTMI_CX
+            if (k[3] < __builtin_huge_val()) stk[(sp++) * 256] = c[3];
+            if (k[2] < __builtin_huge_val()) stk[(sp++) * 256] = c[2];
+            if (k[1] < __builtin_huge_val()) stk[(sp++) * 256] = c[1];
+            if (k[0] < __builtin_huge_val()) {
+                cur = c[0];
+                continue;
             }
+        } else if (cur != kEmptyChild) {
+            const int code = -cur - 1;
+            const int first = code >> 3, end = first + (code & 7);
+            for (int i = first; i < end; i++) tri_test(S, S.tris[i], o, d, r, slot, key, h, vchain);
         }
+        if (sp == 0) break;
+        cur = stk[(--sp) * 256];
     }
 }
 
@@ -458,10 +477,16 @@ __device__ __forceinline__ Hit find_closest(const DevScene& S, int* __restrict__
             d4 d = xform(ob.inv, ob.st, rd);
             const d4 r = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z, 0.0);
             double tmin, tmax;
-            if (!ray_box_ref(o, d, r, ob.bb_min, ob.bb_max, tmin, tmax)) continue;
-            if (tmin > h.t + prune_margin(h.t) || tmax + prune_margin(tmax) < kEps) continue;
-            for (int ci = 0; ci < ob.child_count; ci++)
-                walk_group(S, stk, S.roots[ob.child_base + ci], j, ob.key, o, d, r, h);
+            if (!ray_box_ref(o, d, r, ob.bb_min, ob.bb_max, tmin, tmax)) continue;  // the object's gate (609)
+            int vchain = -1;
+            for (int ci = 0; ci < ob.child_count; ci++) {
+                const RootRec& R = S.root_rec[ob.child_base + ci];
+                double tn;
+                if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
+                             R.hull_mx[2], h.t + prune_margin(h.t), tn))
+                    continue;
+                walk_index(S, stk, R.entry, j, ob.key, o, d, r, h, vchain);
+            }
         }
     }
     return h;
@@ -733,7 +758,7 @@ __device__ __forceinline__ bool bounce_step(const DevScene& S, int* __restrict__
 // grid: x = 4 tiles per block (one 8x8 tile per wave), y = sample chunk.
 // Writes the chunk's RGB sums (A = #samples) to out[(chunk*npix + pixel)*4].
 template <int FL>
-__global__ __launch_bounds__(256, (FL & F_GROUPS) ? 2 : 4) void trace_kernel(DevScene S, uint32_t samples, uint32_t s_begin, uint32_t s_end,
+__global__ __launch_bounds__(256, 4) void trace_kernel(DevScene S, uint32_t samples, uint32_t s_begin, uint32_t s_end,
                                                     uint32_t chunk_len, uint32_t tile_stride, uint32_t tile_offset,
                                                     const double* __restrict__ seeds, const double* __restrict__ sunf,
                                                     double* __restrict__ out) {
