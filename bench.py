@@ -36,6 +36,7 @@ import torch  # noqa: E402  (first: its HIP runtime is the process's, see ptmi/_
 import torch.distributed as dist  # noqa: E402
 
 from ptmi import api, layout  # noqa: E402
+from ptmi import dist as pdist  # noqa: E402
 from tests.scene_inputs import scene_inputs  # noqa: E402
 
 CONFIGS = {
@@ -62,19 +63,32 @@ def cpu_baseline(objs, tris, grps, cam, spp, seeds, budget_s=15.0):
     w = int(np.asarray(cam).reshape(())["width"])
     h = int(np.asarray(cam).reshape(())["height"])
     t2, g2 = layout.pad_empty(tris, grps)
-    # Calibrate on one row at 4 samples, then size the sample (rows x sample range) to the budget.
+    # Calibrate on a centred band of rows at 2 samples, then size the sample to
+    # ~budget_s: the whole frame at n_s samples when the rate allows, else a
+    # centred band of rows at 1 sample.
+    band = max(1, h // 16)
     t0 = time.time()
-    pyoracle.cpu_trace(objs, t2, g2, cam, spp, seeds, row0=h // 2, rows=1, sample_begin=0, sample_end=4,
-                       threads=threads)
-    dt = max(time.time() - t0, 1e-3)
-    rate = w * 4 / dt
-    rows = int(max(1, min(h, budget_s * rate / (w * 16))))
-    n_s = 16
-    row0 = (h - rows) // 2
-    t0 = time.time()
-    pyoracle.cpu_trace(objs, t2, g2, cam, spp, seeds, row0=row0, rows=rows, sample_begin=0, sample_end=n_s,
-                       threads=threads)
-    el = time.time() - t0
+    pyoracle.cpu_trace(objs, t2, g2, cam, spp, seeds, row0=(h - band) // 2, rows=band, sample_begin=0,
+                       sample_end=2, threads=threads)
+    rate = band * w * 2 / max(time.time() - t0, 1e-3)
+    target = budget_s * rate
+    if target >= w * h:
+        rows, n_s = h, int(max(1, min(spp, target // (w * h))))
+    else:
+        rows, n_s = int(max(1, min(h, target // w))), 1
+    for _ in range(3):  # re-size from the last measured run until it fills about half the budget
+        row0 = (h - rows) // 2
+        t0 = time.time()
+        pyoracle.cpu_trace(objs, t2, g2, cam, spp, seeds, row0=row0, rows=rows, sample_begin=0, sample_end=n_s,
+                           threads=threads)
+        el = time.time() - t0
+        if el >= 0.5 * budget_s or (rows == h and n_s == spp):
+            break
+        work = rows * n_s * budget_s / max(el, 1e-3)
+        if rows < h:
+            rows = int(max(1, min(h, work)))
+        else:
+            n_s = int(max(1, min(spp, work // h)))
     return {"value": rows * w * n_s / el / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": "%d rows x %d px x samples [0,%d) of the %d-spp frame (%.1f s)" % (rows, w, n_s, spp, el)}
 
@@ -109,18 +123,12 @@ def main():
     img = torch.empty(npix * 4, dtype=torch.float64, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
 
-    if split == "sample":
-        s0, s1 = rank * S // world, (rank + 1) * S // world
-        t_stride, t_off = 1, 0
-    else:
-        s0, s1 = 0, S
-        t_stride, t_off = world, rank
+    s0, s1, t_stride, t_off = pdist.shard(rank, world, S, split)
 
     def step():
         scene.render(S, s0, s1, seeds.data_ptr(), sums.data_ptr(), tile_stride=t_stride, tile_offset=t_off,
                      chunks=args.chunks, stream=stream)
-        if world > 1:
-            dist.all_reduce(sums)  # RCCL over xGMI: sum of partial framebuffers
+        pdist.reduce_frame(sums)  # RCCL all-reduce over xGMI of the partial framebuffers (N > 1)
         scene.finalize(sums.data_ptr(), img.data_ptr(), S, stream=stream)
 
     for _ in range(args.warmup):

@@ -1,0 +1,52 @@
+"""Multi-GPU frame sharding: one process per GPU, torch.distributed
+over RCCL ("nccl" backend) on a GPU node, gloo in the CPU tests.
+
+Every (pixel, sample) path is independent and depends only on (seed[pixel],
+sample index n, total samples S) (tracer.cl:840-869), so a frame shards with no
+data-path exchange; the only collective is the final sum of the per-rank
+partial framebuffers:
+
+  * sample split -- rank r renders samples [r*S/N, (r+1)*S/N) of every pixel
+    (global n and total S are passed through, so fgi2 = seed/S and the DoF
+    sunflower pattern are those of the full frame);
+  * tile split   -- rank r renders every sample of the 8x8 tiles t with
+    t % N == r (round-robin, balances a mesh-heavy region across ranks) and
+    leaves the other pixels at exactly 0.
+
+Either way the frame is the elementwise SUM of the partial framebuffers
+(ptmi_scene_render writes RGB sums, A = number of samples), reduced with one
+all_reduce(SUM) of W*H*4 doubles and normalised on device (ptmi_finalize).
+For the tile split the sum is exact (x + 0 = x); for the sample split it
+differs from a one-GPU render only by FP64 summation order (~1e-16 relative).
+"""
+TILE = 8  # ptmi_device.h kTile
+
+
+def shard(rank, world, samples, split):
+    """-> (sample_begin, sample_end, tile_stride, tile_offset) of `rank`."""
+    if not (0 <= rank < world):
+        raise ValueError("rank %d outside world %d" % (rank, world))
+    if split == "sample":
+        return rank * samples // world, (rank + 1) * samples // world, 1, 0
+    if split == "tile":
+        return 0, samples, world, rank
+    raise ValueError("split must be 'sample' or 'tile', got %r" % (split,))
+
+
+def tile_owner_mask(width, height, tile_stride, tile_offset):
+    """Boolean (H, W) mask of the pixels a tile-split rank owns: tiles are 8x8,
+    numbered row-major over ceil(W/8) x ceil(H/8) (the kernel's tile index)."""
+    import numpy as np
+    tx = (width + TILE - 1) // TILE
+    ys, xs = np.mgrid[0:height, 0:width]
+    tile = (ys // TILE) * tx + xs // TILE
+    return (tile % tile_stride) == tile_offset
+
+
+def reduce_frame(partial, group=None):
+    """Sum the ranks' partial framebuffers in place (RCCL all-reduce over xGMI
+    on a GPU node; whatever backend `group` uses otherwise).  No-op at N=1."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(partial, op=dist.ReduceOp.SUM, group=group)
+    return partial

@@ -1,0 +1,61 @@
+"""The drop-in boundary on CPU (no GPU calls): libptmi.so loads, exports every
+entry point include/ptmi.h declares with C linkage, carries gfx950 code, and the
+record sizes the header promises are the reference's (ocltracer.go:25-96)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from ptmi import api, layout
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+HEADER = os.path.join(ROOT, "include", "ptmi.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ptmi_[a-z_]+)\s*\(", src)))
+
+
+def _lib_path():
+    if not os.path.exists(api.LIB_PATH):
+        pytest.fail("libptmi.so not built: run __graft_entry__.build() / make -C pathtracer-ocl_amd")
+    return api.LIB_PATH
+
+
+def test_header_declares_the_python_exports():
+    assert _declared() == sorted(api.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib_path()], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    missing = [s for s in _declared() if s not in exported]
+    assert not missing, "not exported with C linkage: %s" % missing
+
+
+def test_library_loads_and_identifies_gfx950():
+    lib = api.load_library()
+    for s in _declared():
+        assert hasattr(lib, s)
+    info = lib.ptmi_build_info().decode()
+    assert "gfx950" in info, info
+    blob = open(_lib_path(), "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the embedded code object targets gfx950
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(FileNotFoundError):
+        api.load_library(str(tmp_path / "libptmi.so"))
+
+
+def test_record_sizes_match_reference_layout():
+    hdr = open(HEADER).read()
+    sizes = dict(re.findall(r"#define (PTMI_\w+_BYTES) (\d+)", hdr))
+    assert int(sizes["PTMI_OBJECT_BYTES"]) == layout.OBJECT_DTYPE.itemsize == 1024
+    assert int(sizes["PTMI_TRIANGLE_BYTES"]) == layout.TRIANGLE_DTYPE.itemsize == 512
+    assert int(sizes["PTMI_GROUP_BYTES"]) == layout.GROUP_DTYPE.itemsize == 256
+    assert int(sizes["PTMI_CAMERA_BYTES"]) == layout.CAMERA_DTYPE.itemsize == 256

@@ -1,0 +1,102 @@
+"""Multi-rank frame sharding on CPU (gloo, world_size 2): the shard arithmetic
+bench.py uses (ptmi/dist.py) partitions the frame, and the all-reduce of the
+ranks' partial framebuffers reproduces the one-process frame.  The partial
+frames come from the CPU oracle (test infrastructure), which renders global
+sample ranges exactly like ptmi_scene_render; the GPU side of the same
+invariances is tests/test_gpu_parity.py::test_sample_split_and_chunking_invariance
+and ::test_tile_split_partitions_frame.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import pyoracle
+from ptmi import dist as pdist
+from ptmi import layout
+from tests.scene_inputs import scene_inputs
+
+W, H, S = 24, 16, 6
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("samples", [1, 5, 2048])
+def test_sample_shards_partition(world, samples):
+    got = []
+    for r in range(world):
+        s0, s1, ts, to = pdist.shard(r, world, samples, "sample")
+        assert (ts, to) == (1, 0) and s0 <= s1
+        got.extend(range(s0, s1))
+    assert got == list(range(samples))
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("w,h", [(1280, 960), (37, 23), (8, 8)])
+def test_tile_shards_partition(world, w, h):
+    cover = np.zeros((h, w), dtype=np.int64)
+    for r in range(world):
+        s0, s1, ts, to = pdist.shard(r, world, 7, "tile")
+        assert (s0, s1, ts) == (0, 7, world)
+        cover += pdist.tile_owner_mask(w, h, ts, to)
+    assert (cover == 1).all()
+
+
+def test_shard_rejects_bad_arguments():
+    with pytest.raises(ValueError):
+        pdist.shard(2, 2, 8, "sample")
+    with pytest.raises(ValueError):
+        pdist.shard(0, 2, 8, "rows")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, split, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        objs, tris, grps, cam = scene_inputs("reference", W, H, 0.15, 1.6)
+        t2, g2 = layout.pad_empty(tris, grps)
+        seeds = layout.seeds_go_float64(W * H, 5)
+        s0, s1, ts, to = pdist.shard(rank, world, S, split)
+        part = pyoracle.cpu_trace(objs, t2, g2, cam, S, seeds, sample_begin=s0, sample_end=s1, threads=1)
+        if s1 - s0 == S:  # a full range comes back normalised: turn it into sums
+            part = part.reshape(-1, 4).copy()
+            part[:, :3] *= S
+            part[:, 3] = S
+            part = part.ravel()
+        if split == "tile":  # this rank's pixels only, the others exactly 0
+            part = part.reshape(H, W, 4) * pdist.tile_owner_mask(W, H, ts, to)[..., None]
+        sums = torch.from_numpy(np.ascontiguousarray(part).ravel())
+        pdist.reduce_frame(sums)
+        if rank == 0:
+            np.save(os.path.join(out_dir, "frame.npy"), sums.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("split", ["sample", "tile"])
+def test_two_rank_frame_matches_single_process(tmp_path, split):
+    if not pyoracle.cpu_available():
+        pytest.skip("oracle not built")
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), split, str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    sums = np.load(tmp_path / "frame.npy").reshape(-1, 4)
+    objs, tris, grps, cam = scene_inputs("reference", W, H, 0.15, 1.6)
+    t2, g2 = layout.pad_empty(tris, grps)
+    full = pyoracle.cpu_trace(objs, t2, g2, cam, S, layout.seeds_go_float64(W * H, 5), threads=1).reshape(-1, 4)
+    assert np.all(sums[:, 3] == S)
+    if split == "tile":  # each pixel comes from one rank (the same conversion to sums): x + 0 = x
+        assert np.array_equal(sums[:, :3], full[:, :3] * S)
+    else:
+        rgb = sums[:, :3] * (1.0 / S)  # ptmi_finalize (tracer.cl:1184-1187)
+        err = np.abs(rgb - full[:, :3]).max()
+        assert err < 1e-12, err  # summation order only
