@@ -55,7 +55,7 @@ typedef struct ptmi_textures {
 /*
  * ptmi_trace -- drop-in for `func Trace(objects []CLObject, triangles []CLTriangle,
  *   groups []CLGroup, deviceIndex, samples int, camera CLCamera, textures,
- *   sphereTextures, cubeTextures []image.Image) []float64`   (ocltracer.go:98-226).
+ *   sphereTextures, cubeTextures []image.Image) []float64`   (ocltracer.go:100-226).
  *
  *  - empty triangle / group slices are allowed (n = 0): the reference pads them
  *    with one zero record (ocltracer.go:106-120), which is equivalent;
