@@ -301,7 +301,17 @@ int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, con
         if (o.reflectivity != 0.0 || o.refractive_index != 1.0) flags |= 4;  // F_MATERIALS
     }
     if (cam.aperture != 0) flags |= 8;                                  // F_DOF
-    if (const char* f = getenv("PTMI_FORCE_FLAGS")) flags = atoi(f) & 15;  // testing: force the generic path
+    // Affine scene (ptmi_kernels.hip dotv): every inverse ends in (+-0, +-0, +-0, 1),
+    // inverse transposes have +-0 in column 3 of rows 0-2, triangle normals have a
+    // finite w.  Otherwise F_PROJ: the generic instantiation with the w lanes.
+    bool affine = cam.inv[12] == 0.0 && cam.inv[13] == 0.0 && cam.inv[14] == 0.0 && cam.inv[15] == 1.0;
+    for (const DevObject& o : objs)
+        affine = affine && o.inv[12] == 0.0 && o.inv[13] == 0.0 && o.inv[14] == 0.0 && o.inv[15] == 1.0 &&
+                 o.inv_t[3] == 0.0 && o.inv_t[7] == 0.0 && o.inv_t[11] == 0.0;
+    for (const DevTriShade& t : st)
+        affine = affine && std::isfinite(t.n1[3]) && std::isfinite(t.n2[3]) && std::isfinite(t.n3[3]);
+    if (!affine) flags |= 16;                                           // F_PROJ
+    if (const char* f = getenv("PTMI_FORCE_FLAGS")) flags = atoi(f) & 31;  // testing: force the generic path
     HIP_TRY(hipSetDevice(device_index));
     ptmi_scene* s = new ptmi_scene();
     s->flags = flags;
@@ -581,3 +591,11 @@ int ptmi_trace(const void* objects, uint32_t n_obj, const void* triangles, uint3
 }
 
 }  // extern "C"
+
+#if PTMI_STATS
+namespace ptmi {
+int stats_read(unsigned long long* out, int reset);
+}
+// DIAGNOSTIC build only: traversal counters (see PTMI_STATS in ptmi_kernels.hip).
+extern "C" int ptmi_stats_read(unsigned long long* out, int reset) { return ptmi::stats_read(out, reset); }
+#endif

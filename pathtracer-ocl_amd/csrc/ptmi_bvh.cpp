@@ -259,6 +259,16 @@ int build_root_index(const uint8_t* tris, const std::vector<DevNode>& nodes, con
     for (const Prim& p : prims)
         for (int k = 0; k < 3; k++) scale = std::max({scale, std::fabs(p.mn[k]), std::fabs(p.mx[k])});
     const double m = 1e-7 * scale + 1e-300;
+    // float box bounds rounded outward (toward -inf / +inf) from the widened doubles
+    auto down = [](double v) {
+        float f = (float)v;
+        return (double)f > v ? std::nextafter(f, -INFINITY) : f;
+    };
+    auto up = [](double v) {
+        float f = (float)v;
+        return (double)f < v ? std::nextafter(f, INFINITY) : f;
+    };
+    float bmax = 0.0f;
     for (int k = 0; k < 3; k++) {
         rec->hull_mn[k] = B.nodes[broot].mn[k] - m;
         rec->hull_mx[k] = B.nodes[broot].mx[k] + m;
@@ -317,18 +327,24 @@ int build_root_index(const uint8_t* tris, const std::vector<DevNode>& nodes, con
             if (i < nk) {
                 const BNode& c = B.nodes[kids[i]];
                 for (int k = 0; k < 3; k++) {
-                    nd.mn[k][i] = c.mn[k] - m;
-                    nd.mx[k][i] = c.mx[k] + m;
+                    nd.mn[k][i] = down(c.mn[k] - m);
+                    nd.mx[k][i] = up(c.mx[k] + m);
+                    bmax = std::max({bmax, std::fabs(nd.mn[k][i]), std::fabs(nd.mx[k][i])});
                 }
                 nd.child[i] = 0;  // patched after emit (emit may grow out.nodes)
             } else {
-                for (int k = 0; k < 3; k++) nd.mn[k][i] = nd.mx[k][i] = 0.0;
+                for (int k = 0; k < 3; k++) nd.mn[k][i] = nd.mx[k][i] = 0.0f;
                 nd.child[i] = kEmptyChild;
             }
         }
         for (int i = 0; i < nk; i++) nd.child[i] = emit(kids[i]);
         out.nodes[slot] = nd;
     }
+    if (!(bmax < 1e30f)) {
+        std::snprintf(err, err_len, "BVH root %d: coordinates too large for the FP32 traversal boxes", root);
+        return PTMI_ERR_UNSUPPORTED;
+    }
+    rec->bmax = bmax;
     return PTMI_OK;
 }
 

@@ -65,15 +65,16 @@ struct alignas(16) ChainBox {
 };
 
 // 4-wide traversal node over one reference root's triangles (ptmi_bvh.cpp).
-// Boxes are widened conservatively; child[i] is a Node4 index (>= 0), a leaf
-// code -((first << 3) | count) - 1 (triangles [first, first + count) of
-// DevScene::tris), or kEmptyChild.
+// Boxes are float, rounded outward from the (slightly widened) double bounds;
+// the kernel's FP32 slab test widens each interval by its own error bound.
+// child[i] is a Node4 index (>= 0), a leaf code -((first << 3) | count) - 1
+// (triangles [first, first + count) of DevScene::tris), or kEmptyChild.
 struct alignas(16) Node4 {
-    double mn[3][4];  // [axis][child]
-    double mx[3][4];
+    float mn[3][4];  // [axis][child]
+    float mx[3][4];
     int32_t child[4];
 };
-static_assert(sizeof(Node4) == 208, "Node4 must stay 208 B");
+static_assert(sizeof(Node4) == 112, "Node4 must stay 112 B");
 constexpr int32_t kEmptyChild = INT32_MIN;
 
 // One BVH root of a group object: the widened hull of all its triangles (the
@@ -81,7 +82,7 @@ constexpr int32_t kEmptyChild = INT32_MIN;
 struct alignas(16) RootRec {
     double hull_mn[3], hull_mx[3];
     int32_t entry;
-    int32_t pad;
+    float bmax;  // max |coordinate| over the root's Node4 boxes (FP32 slab error bound)
 };
 static_assert(sizeof(RootRec) == 64, "RootRec must stay 64 B");
 

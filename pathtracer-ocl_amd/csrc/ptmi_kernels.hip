@@ -21,6 +21,17 @@
 #ifndef PTMI_ABLATE
 #define PTMI_ABLATE 0
 #endif
+// PTMI_STATS: DIAGNOSTIC counting build (make stats) -- tallies traversal events
+// into ptmi_stats[] (read with ptmi_stats_read); the product has PTMI_STATS == 0.
+#ifndef PTMI_STATS
+#define PTMI_STATS 0
+#endif
+#if PTMI_STATS
+__device__ unsigned long long ptmi_stats[8];  // walks, node4, leaves, tri tests, verifies, chain boxes, obj gate pass, rays
+#define PTMI_COUNT(i) atomicAdd(&ptmi_stats[i], 1ull)
+#else
+#define PTMI_COUNT(i) ((void)0)
+#endif
 
 namespace ptmi {
 
@@ -32,6 +43,10 @@ static constexpr double kPi = (double)3.14159265359f;  // tracer.cl:1 (a float l
 // have an empty buffer, or this many lanes are idle waiting for a ray.
 static constexpr int kRefillNeed = 24;
 static constexpr int kRefillStarve = 6;
+#ifndef PTMI_WALK_BATCH
+#define PTMI_WALK_BATCH 24
+#endif
+static constexpr int kWalkBatch = PTMI_WALK_BATCH;  // parked lanes that trigger a wave's BVH walk phase
 
 struct d4 {
     double x, y, z, w;
@@ -71,6 +86,50 @@ __device__ __noinline__ d4 normalize4(d4 v) {
     }
     return scl4(p, rsqrt(d));
 }
+// Affine scenes (F_PROJ clear; ptmi_api.cpp checks at upload that the camera's
+// and every object's inverse end in the row (+-0, +-0, +-0, 1), that the inverse
+// transposes' column 3 is +-0 in rows 0-2 and that triangle normals are finite):
+// points then carry w == 1 and directions w == 0 along every path, so every
+// w-lane term of the reference's double4 arithmetic is an exact no-op (a +-0
+// product or m * 1), up to the sign of an exact-zero result, which nothing
+// observes.  With A = true the helpers below skip the w lane (and all w values
+// become dead code); with A = false they are the literal double4 arithmetic.
+template <bool A>
+__device__ __forceinline__ double dotv(d4 a, d4 b) {  // dot of two directions (w == 0 when A)
+    double d = a.x * b.x;
+    d = fma(a.y, b.y, d);
+    d = fma(a.z, b.z, d);
+    return A ? d : fma(a.w, b.w, d);
+}
+// normalize of a direction, affine case: the w lane is 0 in and out.
+__device__ __noinline__ d4 normalize3(double x, double y, double z) {
+    if (x == 0.0 && y == 0.0 && z == 0.0) return mk(x, y, z, 0.0);
+    double d = x * x;
+    d = fma(y, y, d);
+    d = fma(z, z, d);
+    double px = x, py = y, pz = z;
+    if (d < 0x1p-1022) {
+        px = x * 0x1p563, py = y * 0x1p563, pz = z * 0x1p563;
+        d = fma(pz, pz, fma(py, py, px * px));
+    } else if (d == __builtin_inf()) {
+        px = x * 0x1p-514, py = y * 0x1p-514, pz = z * 0x1p-514;
+        d = fma(pz, pz, fma(py, py, px * px));
+        if (d == __builtin_inf()) {
+            px = copysign(isinf(px) ? 1.0 : 0.0, px);
+            py = copysign(isinf(py) ? 1.0 : 0.0, py);
+            pz = copysign(isinf(pz) ? 1.0 : 0.0, pz);
+            d = fma(pz, pz, fma(py, py, px * px));
+        }
+    }
+    const double s = rsqrt(d);
+    return mk(px * s, py * s, pz * s, 0.0);
+}
+template <bool A>
+__device__ __forceinline__ d4 normv(d4 v) {
+    if constexpr (A) return normalize3(v.x, v.y, v.z);
+    else return normalize4(v);
+}
+
 // maxX / minX (tracer.cl:110-111): OpenCL max/min -> maxnum/minnum.
 __device__ __forceinline__ double max3(double a, double b, double c) { return fmax(fmax(a, b), c); }
 __device__ __forceinline__ double min3(double a, double b, double c) { return fmin(fmin(a, b), c); }
@@ -95,6 +154,23 @@ __device__ __forceinline__ d4 xform_st(const double* __restrict__ m, d4 v) {
 __device__ __forceinline__ d4 xform(const double* __restrict__ m, bool st, d4 v) {
     return st ? xform_st(m, v) : mat_mul(m, v);
 }
+// mul(m, point) / mul(m, direction): in the affine case m * 1 == m and
+// m * 0 == +-0 make the w column an exact add of m[3] / a no-op, and row 3 is dead.
+template <bool A>
+__device__ __forceinline__ d4 xpt(const double* __restrict__ m, bool st, d4 v) {
+    if constexpr (!A) return xform(m, st, v);
+    if (st) return mk(m[0] * v.x + m[3], m[5] * v.y + m[7], m[10] * v.z + m[11], 1.0);
+    return mk(((m[0] * v.x + m[1] * v.y) + m[2] * v.z) + m[3], ((m[4] * v.x + m[5] * v.y) + m[6] * v.z) + m[7],
+              ((m[8] * v.x + m[9] * v.y) + m[10] * v.z) + m[11], 1.0);
+}
+template <bool A>
+__device__ __forceinline__ d4 xdir(const double* __restrict__ m, bool st, d4 v) {
+    if constexpr (!A) return xform(m, st, v);
+    if (st) return mk(m[0] * v.x, m[5] * v.y, m[10] * v.z, 0.0);
+    return mk((m[0] * v.x + m[1] * v.y) + m[2] * v.z, (m[4] * v.x + m[5] * v.y) + m[6] * v.z,
+              (m[8] * v.x + m[9] * v.y) + m[10] * v.z, 0.0);
+}
+
 // Row 1 of mul() only (intersectPlane reads nothing else, tracer.cl:478-483).
 __device__ __forceinline__ double row1(const double* __restrict__ m, bool st, d4 v) {
     return st ? m[5] * v.y + m[7] * v.w : ((m[4] * v.x + m[5] * v.y) + m[6] * v.z) + m[7] * v.w;
@@ -181,7 +257,8 @@ enum : int {
     F_CYLCUBE = 2,    // cylinders or cubes present
     F_MATERIALS = 4,  // reflectivity != 0 or refractive index != 1 somewhere
     F_DOF = 8,        // camera aperture != 0
-    F_ALL = 15
+    F_ALL = 15,
+    F_PROJ = 16       // not affine (see dotv): the literal double4 arithmetic, generic path only
 };
 
 // intersectRayWithBox (tracer.cl:270-280) returning the line's slab interval.
@@ -243,10 +320,10 @@ __device__ __forceinline__ bool ray_box_ref(d4 o, d4 d, d4 r, const double* mn, 
 
 // Moller-Trumbore (tracer.cl:640-675) on the 3 live components: the w terms of
 // the reference's dot() products multiply a cross() result whose w is exactly 0.
-__device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o, d4 d, d4 r);
+__device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o, d4 d);
 
-__device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 o, d4 d, d4 r, int slot, int key,
-                                         Hit& h, int& vchain) {
+__device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 o, d4 d, int slot, int key, Hit& h,
+                                         int& vchain) {
     const double e1x = T.e1[0], e1y = T.e1[1], e1z = T.e1[2];
     const double e2x = T.e2[0], e2y = T.e2[1], e2z = T.e2[2];
     // dirCrossE2 = cross(d, e2)
@@ -283,7 +360,9 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 
         // its gate chain (root -> its node) passes the exact line-box tests.
         const int c = T.chain;
         if (c != vchain) {
-            if (!verify_chain(S, c, o, d, r)) return;
+#if !(defined(PTMI_EXP) && (PTMI_EXP & 8))
+            if (!verify_chain(S, c, o, d)) return;
+#endif
             vchain = c;
         }
         h.t = t;
@@ -300,10 +379,13 @@ static constexpr int kStack = 24;  // per-lane LDS traversal stack (3 pushes x B
 // The reference's gate for one triangle: every reference node on the path from
 // the walked root to the triangle's node passes intersectRayWithBox
 // (tracer.cl:617-719).  Boxes are contiguous, so their loads are independent.
-__device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o, d4 d, d4 r) {
+__device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o, d4 d) {
+    const d4 r = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z, 0.0);  // recomputed: rare, and keeps r out of the walk
     const ChainBox* B = S.chains + (chain >> 5);
     const int len = chain & 31;
+    PTMI_COUNT(4);
     for (int i = 0; i < len; i++) {
+        PTMI_COUNT(5);
         double a, b;
         if (!ray_box_ref(o, d, r, B[i].mn, B[i].mx, a, b)) return false;
     }
@@ -327,29 +409,54 @@ __device__ __forceinline__ bool cull_box(d4 o, d4 r, double mnx, double mny, dou
 // child first, the others pushed far-to-near.  Which triangles are FOUND does
 // not depend on the visiting order or the widened boxes (every triangle that
 // can produce a winning t is reached); ties resolve through better_tri.
-__device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, int entry, int slot, int key,
-                                           d4 o, d4 d, d4 r, Hit& h, int& vchain) {
+__device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const RootRec& R, int slot,
+                                           int key, d4 o, d4 d, Hit& h, int& vchain) {
+    // FP32 slab tests.  With of = (float)o, rf = (float)(1/d) (|rf| clamped to
+    // 1e30) and t' = fma(b, rf, -RN(of*rf)), the computed slab bound differs from
+    // the exact (b - o)/d by at most 2^-23 |r| (|b| + 2|o|) (FP32 roundings of o,
+    // r, the product and the fma); each axis interval is widened by 4x that, so
+    // the test only rejects boxes the exact line misses.
+    float of[3], rf[3], ofr[3], dt[3];
+    const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+    float omax = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        of[a] = (float)oo[a];
+        const float r = (float)(1.0 / dd[a]);
+        rf[a] = fminf(fmaxf(r, -1e30f), 1e30f);  // NaN stays NaN
+        ofr[a] = of[a] * rf[a];
+        omax = fmaxf(omax, fabsf(of[a]));
+    }
+    const float E = 0x1p-21f * (R.bmax + 2.0f * omax) + 0x1p-120f;
+#pragma unroll
+    for (int a = 0; a < 3; a++) dt[a] = E * fabsf(rf[a]);
     int sp = 0;
-    int cur = entry;
+    int cur = R.entry;
+    PTMI_COUNT(0);
     while (true) {
         if (cur >= 0) {
+            PTMI_COUNT(1);
             const Node4& N = S.nodes4[cur];
-            const double lim = h.t + prune_margin(h.t);
-            double k[4];
+            const double limd = h.t + prune_margin(h.t);
+            const float lim = (float)limd * (1.0f + 0x1p-22f) + 0x1p-100f;  // >= limd
+            float k[4];
             int c[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                double tn;
                 c[i] = N.child[i];
-                const bool cull = cull_box(o, r, N.mn[0][i], N.mn[1][i], N.mn[2][i], N.mx[0][i], N.mx[1][i],
-                                           N.mx[2][i], lim, tn) ||
-                                  c[i] == kEmptyChild;
-                k[i] = cull ? __builtin_huge_val() : fmax(tn, -__builtin_huge_val());  // NaN -> -inf
+                const float ax = fmaf(N.mn[0][i], rf[0], -ofr[0]), bx = fmaf(N.mx[0][i], rf[0], -ofr[0]);
+                const float ay = fmaf(N.mn[1][i], rf[1], -ofr[1]), by = fmaf(N.mx[1][i], rf[1], -ofr[1]);
+                const float az = fmaf(N.mn[2][i], rf[2], -ofr[2]), bz = fmaf(N.mx[2][i], rf[2], -ofr[2]);
+                const float tn = fmaxf(fmaxf(fminf(ax, bx) - dt[0], fminf(ay, by) - dt[1]), fminf(az, bz) - dt[2]);
+                const float tf = fminf(fminf(fmaxf(ax, bx) + dt[0], fmaxf(ay, by) + dt[1]), fmaxf(az, bz) + dt[2]);
+                // (NaN bounds -- a NaN ray -- fail every test: the child is entered.)
+                const bool cull = tn > tf || tn > lim || tf < 0.0f || c[i] == kEmptyChild;
+                k[i] = cull ? __builtin_huge_valf() : fmaxf(tn, -__builtin_huge_valf());  // NaN -> -inf
             }
             // sort (k, c) ascending: 5 compare-exchanges
 #define PTMI_CX(a, b)                                      \
     if (k[b] < k[a]) {                                     \
-        const double tk = k[a];                            \
+        const float tk = k[a];                             \
         k[a] = k[b];                                       \
         k[b] = tk;                                         \
         const int tc = c[a];                               \
@@ -358,17 +465,23 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
     }
             PTMI_CX(0, 1) PTMI_CX(2, 3) PTMI_CX(0, 2) PTMI_CX(1, 3) PTMI_CX(1, 2)
 #undef PTMI_CX
-            if (k[3] < __builtin_huge_val()) stk[(sp++) * 256] = c[3];
-            if (k[2] < __builtin_huge_val()) stk[(sp++) * 256] = c[2];
-            if (k[1] < __builtin_huge_val()) stk[(sp++) * 256] = c[1];
-            if (k[0] < __builtin_huge_val()) {
+            if (k[3] < __builtin_huge_valf()) stk[(sp++) * 256] = c[3];
+            if (k[2] < __builtin_huge_valf()) stk[(sp++) * 256] = c[2];
+            if (k[1] < __builtin_huge_valf()) stk[(sp++) * 256] = c[1];
+            if (k[0] < __builtin_huge_valf()) {
                 cur = c[0];
                 continue;
             }
         } else if (cur != kEmptyChild) {
             const int code = -cur - 1;
             const int first = code >> 3, end = first + (code & 7);
-            for (int i = first; i < end; i++) tri_test(S, S.tris[i], o, d, r, slot, key, h, vchain);
+            PTMI_COUNT(2);
+            for (int i = first; i < end; i++) {
+                PTMI_COUNT(3);
+#if !(defined(PTMI_EXP) && (PTMI_EXP & 4))
+                tri_test(S, S.tris[i], o, d, slot, key, h, vchain);
+#endif
+            }
         }
         if (sp == 0) break;
         cur = stk[(--sp) * 256];
@@ -386,11 +499,12 @@ __device__ __forceinline__ void consider_sel(Hit& h, double t, int obj, int key)
 }
 
 // intersectSphere (tracer.cl:448-476) on an object-space ray.
+template <bool A>
 __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int key) {
-    d4 vtc = mk(o.x - 0.0, o.y - 0.0, o.z - 0.0, o.w - 1.0);
-    double a = dot4(d, d);
-    double b = 2.0 * dot4(d, vtc);
-    double c = dot4(vtc, vtc) - 1.0;
+    d4 vtc = mk(o.x - 0.0, o.y - 0.0, o.z - 0.0, A ? 0.0 : o.w - 1.0);
+    double a = dotv<A>(d, d);
+    double b = 2.0 * dotv<A>(d, vtc);
+    double c = dotv<A>(vtc, vtc) - 1.0;
     double disc = (b * b) - 4 * a * c;
     if (disc > 0.0) {
         // a > 0 and sq >= 0 give t1 <= t2 after rounding (rounding is monotonic),
@@ -409,34 +523,40 @@ __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int ke
 // findClosestIntersection (tracer.cl:537-742), one loop per object type.  Loop
 // indices are wave-uniform, so object data arrives through scalar loads.
 template <int FL>
-__device__ __forceinline__ Hit find_closest(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd) {
+__device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 rd) {
+    constexpr bool A = !(FL & F_PROJ);
     Hit h{1024.0, -1, -1, -1, 0.0, 0.0};
     for (int p = 0; p < ((PTMI_ABLATE & 8) ? 0 : S.n_planes); p++) {  // intersectPlane (478-483): row 1 only
         const PlaneRec& P = S.planes[p];
-        const double oy = ((P.row1[0] * ro.x + P.row1[1] * ro.y) + P.row1[2] * ro.z) + P.row1[3] * ro.w;
-        const double dy = ((P.row1[0] * rd.x + P.row1[1] * rd.y) + P.row1[2] * rd.z) + P.row1[3] * rd.w;
+        const double oy = ((P.row1[0] * ro.x + P.row1[1] * ro.y) + P.row1[2] * ro.z) + (A ? P.row1[3] : P.row1[3] * ro.w);
+        const double dy0 = (P.row1[0] * rd.x + P.row1[1] * rd.y) + P.row1[2] * rd.z;
+        const double dy = A ? dy0 : dy0 + P.row1[3] * rd.w;
         const double q = -oy / dy;
         consider_sel(h, fabs(dy) > kEps ? q : 0.0, P.slot, P.key);
     }
     for (int q = 0; q < ((PTMI_ABLATE & 16) ? 0 : S.n_spheres_st); q++) {  // scale+translate spheres
         const SphereRec& Q = S.spheres[q];
-        const d4 o = mk(Q.m0 * ro.x + Q.m3 * ro.w, Q.m5 * ro.y + Q.m7 * ro.w, Q.m10 * ro.z + Q.m11 * ro.w,
-                        Q.m15 * ro.w);
-        const d4 d = mk(Q.m0 * rd.x + Q.m3 * rd.w, Q.m5 * rd.y + Q.m7 * rd.w, Q.m10 * rd.z + Q.m11 * rd.w,
-                        Q.m15 * rd.w);
-        sphere_test(h, o, d, Q.slot, Q.key);
+        d4 o, d;
+        if constexpr (A) {
+            o = mk(Q.m0 * ro.x + Q.m3, Q.m5 * ro.y + Q.m7, Q.m10 * ro.z + Q.m11, 1.0);
+            d = mk(Q.m0 * rd.x, Q.m5 * rd.y, Q.m10 * rd.z, 0.0);
+        } else {
+            o = mk(Q.m0 * ro.x + Q.m3 * ro.w, Q.m5 * ro.y + Q.m7 * ro.w, Q.m10 * ro.z + Q.m11 * ro.w, Q.m15 * ro.w);
+            d = mk(Q.m0 * rd.x + Q.m3 * rd.w, Q.m5 * rd.y + Q.m7 * rd.w, Q.m10 * rd.z + Q.m11 * rd.w, Q.m15 * rd.w);
+        }
+        sphere_test<A>(h, o, d, Q.slot, Q.key);
     }
     int j = S.run_end[0];
     for (; j < S.run_end[1]; j++) {  // spheres with other matrices
         const DevObject& ob = S.objs[j];
         if (ob.st) continue;  // in S.spheres
-        sphere_test(h, mat_mul(ob.inv, ro), mat_mul(ob.inv, rd), j, ob.key);
+        sphere_test<A>(h, xpt<A>(ob.inv, false, ro), xdir<A>(ob.inv, false, rd), j, ob.key);
     }
     if (FL & F_CYLCUBE) {
         for (; j < S.run_end[2]; j++) {  // cylinders: intersectCylinder (396-446), caps disabled
             const DevObject& ob = S.objs[j];
-            d4 o = xform(ob.inv, ob.st, ro);
-            d4 d = xform(ob.inv, ob.st, rd);
+            d4 o = xpt<A>(ob.inv, ob.st, ro);
+            d4 d = xdir<A>(ob.inv, ob.st, rd);
             double a = d.x * d.x + d.z * d.z;
             if (!(fabs(a) < kEps)) {
                 double b = 2 * o.x * d.x + 2 * o.z * d.z;
@@ -457,8 +577,8 @@ __device__ __forceinline__ Hit find_closest(const DevScene& S, int* __restrict__
         }
         for (; j < S.run_end[3]; j++) {  // cubes: intersectCube (378-394)
             const DevObject& ob = S.objs[j];
-            d4 o = xform(ob.inv, ob.st, ro);
-            d4 d = xform(ob.inv, ob.st, rd);
+            d4 o = xpt<A>(ob.inv, ob.st, ro);
+            d4 d = xdir<A>(ob.inv, ob.st, rd);
             double x0, x1, y0, y1, z0, z1;
             check_axis(o.x, d.x, -1.0, 1.0, x0, x1);
             check_axis(o.y, d.y, -1.0, 1.0, y0, y1);
@@ -470,31 +590,66 @@ __device__ __forceinline__ Hit find_closest(const DevScene& S, int* __restrict__
             }
         }
     }
-    if (FL & F_GROUPS) {
-        for (j = S.run_end[3]; j < S.run_end[4]; j++) {  // groups (598-720)
-            const DevObject& ob = S.objs[j];
-            d4 o = xform(ob.inv, ob.st, ro);
-            d4 d = xform(ob.inv, ob.st, rd);
-            const d4 r = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z, 0.0);
-            double tmin, tmax;
-            if (!ray_box_ref(o, d, r, ob.bb_min, ob.bb_max, tmin, tmax)) continue;  // the object's gate (609)
-            int vchain = -1;
-            for (int ci = 0; ci < ob.child_count; ci++) {
-                const RootRec& R = S.root_rec[ob.child_base + ci];
-                double tn;
-                if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
-                             R.hull_mx[2], h.t + prune_margin(h.t), tn))
-                    continue;
-                walk_index(S, stk, R.entry, j, ob.key, o, d, r, h, vchain);
-            }
-        }
-    }
     return h;
 }
 
+// Groups (tracer.cl:598-720), split in two so a wave can defer the walks
+// (see trace_kernel): group_needs_walk is the cheap part -- the object's exact
+// gate and the roots' hull culls against the current best -- and group_walks
+// walks every root that survives, updating h.
+template <bool A>
+__device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd, const Hit& h) {
+#if defined(PTMI_EXP) && (PTMI_EXP & 2)
+    return false;
+#endif
+    for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
+        const DevObject& ob = S.objs[j];
+        const d4 o = xpt<A>(ob.inv, ob.st, ro);
+        const d4 d = xdir<A>(ob.inv, ob.st, rd);
+        const d4 r = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z, 0.0);
+        double tmin, tmax;
+        if (!ray_box_ref(o, d, r, ob.bb_min, ob.bb_max, tmin, tmax)) continue;
+        for (int ci = 0; ci < ob.child_count; ci++) {
+            const RootRec& R = S.root_rec[ob.child_base + ci];
+            double tn;
+            if (!cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
+                          R.hull_mx[2], h.t + prune_margin(h.t), tn))
+                return true;
+        }
+    }
+    return false;
+}
+
+template <bool A>
+__device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
+#if defined(PTMI_EXP) && (PTMI_EXP & 1)
+    return;
+#endif
+    for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
+        const DevObject& ob = S.objs[j];
+        const d4 o = xpt<A>(ob.inv, ob.st, ro);
+        const d4 d = xdir<A>(ob.inv, ob.st, rd);
+        const d4 r = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z, 0.0);
+        double tmin, tmax;
+        PTMI_COUNT(7);
+        if (!ray_box_ref(o, d, r, ob.bb_min, ob.bb_max, tmin, tmax)) continue;  // the object's gate (609)
+        PTMI_COUNT(6);
+        int vchain = -1;
+        for (int ci = 0; ci < ob.child_count; ci++) {
+            const RootRec& R = S.root_rec[ob.child_base + ci];
+            double tn;
+            if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
+                         R.hull_mx[2], h.t + prune_margin(h.t), tn))
+                continue;
+            walk_index(S, stk, R, j, ob.key, o, d, h, vchain);
+        }
+    }
+}
+
 // schlick (tracer.cl:485-505)
+template <bool A>
 __device__ __noinline__ double schlick(d4 eye, d4 nrm, double n1, double n2) {
-    double c = dot4(eye, nrm);
+    double c = dotv<A>(eye, nrm);
     if (n1 > n2) {
         double n = n1 / n2;
         double s2 = (n * n) * (1.0 - (c * c));
@@ -507,18 +662,21 @@ __device__ __noinline__ double schlick(d4 eye, d4 nrm, double n1, double n2) {
 }
 
 // computeRefractedRay (tracer.cl:507-533)
+template <bool A>
 __device__ __noinline__ d4 refracted(d4 eye, d4 nrm, double n1, double n2) {
     double nr = n1 / n2;
-    double ci = dot4(eye, nrm);
+    double ci = dotv<A>(eye, nrm);
     double s2 = (nr * nr) * (1.0 - (ci * ci));
     if (s2 > 1.0) return mk(0, 0, 0, 0);
     double ct = sqrt(1.0 - s2);
     return sub4(scl4(nrm, (nr * ci) - ct), scl4(eye, nr));
 }
 
-__device__ __forceinline__ d4 reflect(d4 rd, d4 nv) { return sub4(rd, scl4(scl4(nv, 2.0), dot4(rd, nv))); }
+template <bool A>
+__device__ __forceinline__ d4 reflect(d4 rd, d4 nv) { return sub4(rd, scl4(scl4(nv, 2.0), dotv<A>(rd, nv))); }
 
 // randomVectorInHemisphere (tracer.cl:348-366); x, y, z hold float-valued doubles.
+template <bool A>
 __device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float fz) {
     double rand1 = 2.0 * kPi * (double)noise3d(fx, fy, fz);
     double rand2 = (double)noise3d(fy, fz, fx);
@@ -527,7 +685,7 @@ __device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float
     // exactly (up to the sign of exact zeros) to component moves:
     //   cross((0,1,0,0), n) = (n.z, 0, -n.x, 0),  cross((1,0,0,0), n) = (0, -n.z, n.y, 0)
     d4 c = fabs(nv.x) > 0.1 ? mk(nv.z, 0.0, -nv.x, 0.0) : mk(0.0, -nv.z, nv.y, 0.0);
-    d4 u = normalize4(c);
+    d4 u = normv<A>(c);
     d4 v = cross4(nv, u);
     double sr, cr;
     if (PTMI_ABLATE & 4) {
@@ -577,7 +735,7 @@ __device__ __forceinline__ CamConst cam_const(const DevCamera& cam) {
 // rayForPixel (tracer.cl:745-779).  With DoF the aperture offset
 // sunflower(S, 2, n) depends only on n: it is read from a per-frame table
 // (sunflower_kernel) made with the same arithmetic.
-template <bool kDof>
+template <bool kDof, bool A>
 __device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, const CamConst& cc, const double* __restrict__ sunf,
                                               unsigned x, unsigned y, float rx, float ry, int sample, d4& ro,
                                               d4& rd) {
@@ -586,9 +744,11 @@ __device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, const CamCon
     const double a = cam.half_width - xo, b = cam.half_height - yo;
     const double* m = cam.inv;
     d4 pixel = mk(((m[0] * a + m[1] * b) + cc.nm2[0]) + cc.m3[0], ((m[4] * a + m[5] * b) + cc.nm2[1]) + cc.m3[1],
-                  ((m[8] * a + m[9] * b) + cc.nm2[2]) + cc.m3[2], ((m[12] * a + m[13] * b) + cc.nm2[3]) + cc.m3[3]);
+                  ((m[8] * a + m[9] * b) + cc.nm2[2]) + cc.m3[2],
+                  A ? 1.0 : ((m[12] * a + m[13] * b) + cc.nm2[3]) + cc.m3[3]);
     d4 origin = cc.origin;
-    d4 dir = (PTMI_ABLATE & 2) ? sub4(pixel, origin) : normalize4(sub4(pixel, origin));
+    if (A) origin.w = 1.0;
+    d4 dir = (PTMI_ABLATE & 2) ? sub4(pixel, origin) : normv<A>(sub4(pixel, origin));
     if (kDof && cam.aperture != 0) {
         d4 pos = add4(origin, scl4(dir, cam.focal_length));
         const double sx = sunf[2 * sample], sy = sunf[2 * sample + 1];
@@ -618,6 +778,7 @@ struct PathState {
     bool dead;
 };
 
+template <bool A>
 __device__ __forceinline__ void start_path(PathState& P, d4 ro, d4 rd) {
     P.ro = ro;
     P.rd = rd;
@@ -625,16 +786,16 @@ __device__ __forceinline__ void start_path(PathState& P, d4 ro, d4 rd) {
     P.ar = P.ag = P.ab = 0.0;
     P.b = P.k = P.effective = 0;
     P.inside = P.done = false;
-    P.dead = !(isfinite(ro.x) && isfinite(ro.y) && isfinite(ro.z) && isfinite(ro.w) && isfinite(rd.x) &&
-               isfinite(rd.y) && isfinite(rd.z) && isfinite(rd.w));
+    P.dead = !(isfinite(ro.x) && isfinite(ro.y) && isfinite(ro.z) && (A || isfinite(ro.w)) && isfinite(rd.x) &&
+               isfinite(rd.y) && isfinite(rd.z) && (A || isfinite(rd.w)));
 }
 
 // One bounce (tracer.cl:884-1110).  Returns true when the path has ended.
+// One bounce of the path given its closest hit h (tracer.cl:886-1110 after
+// findClosestIntersection).  Returns true when the path has ended.
 template <int FL>
-__device__ __forceinline__ bool bounce_step(const DevScene& S, int* __restrict__ stk, PathState& P, float fgi,
-                                            uint32_t n) {
-    if (P.dead) return true;
-    Hit h = find_closest<FL>(S, stk, P.ro, P.rd);
+__device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, const Hit& h, float fgi, uint32_t n) {
+    constexpr bool A = !(FL & F_PROJ);
     if (h.obj < 0) return true;  // a miss repeats identically until b == 10 in the reference
     const DevObject& ob = S.objs[h.obj];
     const int type = ob.type;
@@ -648,16 +809,16 @@ __device__ __forceinline__ bool bounce_step(const DevScene& S, int* __restrict__
     } else {
         d4 on;
         if (type == 1) {
-            d4 lp = xform(ob.inv, ob.st, pos);
-            on = mk(lp.x - 0.0, lp.y - 0.0, lp.z - 0.0, lp.w - 1.0);
+            d4 lp = xpt<A>(ob.inv, ob.st, pos);
+            on = mk(lp.x - 0.0, lp.y - 0.0, lp.z - 0.0, A ? 0.0 : lp.w - 1.0);
         } else if ((FL & F_CYLCUBE) && type == 2) {
-            d4 lp = xform(ob.inv, ob.st, pos);
+            d4 lp = xpt<A>(ob.inv, ob.st, pos);
             double dist = lp.x * lp.x + lp.z * lp.z;  // pow(v, 2) folds to v*v
             if (dist < 1 && lp.y >= ob.max_y - kEps) on = mk(0.0, 1.0, 0.0, 0.0);
             else if (dist < 1 && lp.y <= ob.min_y + kEps) on = mk(0.0, -1.0, 0.0, 0.0);
             else on = mk(lp.x, 0.0, lp.z, 0.0);
         } else if ((FL & F_CYLCUBE) && type == 3) {
-            d4 lp = xform(ob.inv, ob.st, pos);
+            d4 lp = xpt<A>(ob.inv, ob.st, pos);
             double mc = max3(fabs(lp.x), fabs(lp.y), fabs(lp.z));
             if (mc == fabs(lp.x)) on = mk(lp.x, 0.0, 0.0, 0.0);
             else if (mc == fabs(lp.y)) on = mk(0.0, lp.y, 0.0, 0.0);
@@ -671,45 +832,50 @@ __device__ __forceinline__ bool bounce_step(const DevScene& S, int* __restrict__
         if (ob.invt_diag) {
             nv = mk(it[0] * on.x, it[5] * on.y, it[10] * on.z, 0.0);
         } else {
-            nv.x = ((it[0] * on.x + it[1] * on.y) + it[2] * on.z) + it[3] * on.w;
-            nv.y = ((it[4] * on.x + it[5] * on.y) + it[6] * on.z) + it[7] * on.w;
-            nv.z = ((it[8] * on.x + it[9] * on.y) + it[10] * on.z) + it[11] * on.w;
+            nv.x = (it[0] * on.x + it[1] * on.y) + it[2] * on.z;
+            nv.y = (it[4] * on.x + it[5] * on.y) + it[6] * on.z;
+            nv.z = (it[8] * on.x + it[9] * on.y) + it[10] * on.z;
+            if constexpr (!A) {  // affine: it[3], it[7], it[11] are +-0 and on.w is finite
+                nv.x = nv.x + it[3] * on.w;
+                nv.y = nv.y + it[7] * on.w;
+                nv.z = nv.z + it[11] * on.w;
+            }
             nv.w = 0.0;
         }
-        nv = normalize4(nv);
+        nv = normv<A>(nv);
     }
-    if (dot4(eye, nv) < 0.0) nv = scl4(nv, -1.0);
+    if (dotv<A>(eye, nv) < 0.0) nv = scl4(nv, -1.0);
     d4 over = add4(pos, scl4(nv, kEps));
     double cosine = 1.0;
     bool entering = false, exiting = false, reflecting = false;
     // Material decision (tracer.cl:973-1061)
     if ((FL & F_MATERIALS) && ob.reflectivity != 0.0 && noise3d(fgi, (float)n, (float)b) < ob.reflectivity) {
-        P.rd = reflect(P.rd, nv);
+        P.rd = reflect<A>(P.rd, nv);
         reflecting = true;
     } else if ((FL & F_MATERIALS) && ob.refractive_index == -1.0) {
-        if (schlick(eye, nv, 1.0, 1.5) < noise3d(fgi, (float)(n * n), (float)b)) {
+        if (schlick<A>(eye, nv, 1.0, 1.5) < noise3d(fgi, (float)(n * n), (float)b)) {
             over = sub4(pos, scl4(nv, kEps));
         } else {
-            P.rd = reflect(P.rd, nv);
+            P.rd = reflect<A>(P.rd, nv);
             reflecting = true;
         }
     } else if ((FL & F_MATERIALS) && ob.refractive_index != 1.0) {
         const double ri = ob.refractive_index;
         const bool in = P.inside;
-        const double sch = in ? schlick(eye, nv, ri, 1.0) : schlick(eye, nv, 1.0, ri);
+        const double sch = in ? schlick<A>(eye, nv, ri, 1.0) : schlick<A>(eye, nv, 1.0, ri);
         if (sch < noise3d(fgi, (float)(n * n), (float)b)) {
-            P.rd = in ? refracted(eye, nv, ri, 1.0) : refracted(eye, nv, 1.0, ri);
+            P.rd = in ? refracted<A>(eye, nv, ri, 1.0) : refracted<A>(eye, nv, 1.0, ri);
             over = sub4(pos, scl4(nv, kEps));
             entering = !in;
             exiting = in;
             P.inside = !in;
         } else {
-            P.rd = reflect(P.rd, nv);
+            P.rd = reflect<A>(P.rd, nv);
             reflecting = true;
         }
     } else {
-        P.rd = random_hemisphere(nv, fgi, (float)b, (float)n);
-        cosine = dot4(P.rd, nv);
+        P.rd = random_hemisphere<A>(nv, fgi, (float)b, (float)n);
+        cosine = dotv<A>(P.rd, nv);
     }
     P.ro = over;
     // Bounce record + reduction step (tracer.cl:1071-1096, 1148-1175).
@@ -758,7 +924,13 @@ __device__ __forceinline__ bool bounce_step(const DevScene& S, int* __restrict__
 // grid: x = 4 tiles per block (one 8x8 tile per wave), y = sample chunk.
 // Writes the chunk's RGB sums (A = #samples) to out[(chunk*npix + pixel)*4].
 template <int FL>
-__global__ __launch_bounds__(256, 4) void trace_kernel(DevScene S, uint32_t samples, uint32_t s_begin, uint32_t s_end,
+#ifndef PTMI_WAVES
+#define PTMI_WAVES 4        // waves/SIMD the register allocation targets (scenes without groups)
+#endif
+#ifndef PTMI_WAVES_GROUPS
+#define PTMI_WAVES_GROUPS 3  // ... and with BVH groups (the walk needs more registers; 4 spills)
+#endif
+__global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, uint32_t s_begin, uint32_t s_end,
                                                     uint32_t chunk_len, uint32_t tile_stride, uint32_t tile_offset,
                                                     const double* __restrict__ seeds, const double* __restrict__ sunf,
                                                     double* __restrict__ out) {
@@ -772,6 +944,7 @@ __global__ __launch_bounds__(256, 4) void trace_kernel(DevScene S, uint32_t samp
     const int px = (tile % tiles_x) * kTile + (lane & 7);
     const int py = (tile / tiles_x) * kTile + (lane >> 3);
     if (px >= W || py >= H) return;
+    constexpr bool A = !(FL & F_PROJ);
     const uint32_t i = (uint32_t)py * (uint32_t)W + (uint32_t)px;
     const uint32_t c0 = s_begin + blockIdx.y * chunk_len;
     const uint32_t c1 = min(s_end, c0 + chunk_len);
@@ -787,7 +960,9 @@ __global__ __launch_bounds__(256, 4) void trace_kernel(DevScene S, uint32_t samp
     // transform) on nearly every bounce iteration with ~1/5 of the lanes active.
     // Per lane the samples are still traced in order n = c0, c0+1, ..., so the
     // arithmetic and the order of `colors +=` are unchanged.
-    __shared__ d4 cam_ro[256], cam_rd[256];
+    // SoA, component c of lane t at [c * 256 + t]; affine scenes keep no w lanes.
+    constexpr int kCamComp = A ? 6 : 8;
+    __shared__ double cam_lds[kCamComp * 256];
     const int tid = threadIdx.x;
     // Per-lane BVH traversal stacks, lane-interleaved (entry k of lane t at
     // [k * 256 + t]) so a wave's pushes and pops hit 64 consecutive dwords.
@@ -795,8 +970,9 @@ __global__ __launch_bounds__(256, 4) void trace_kernel(DevScene S, uint32_t samp
     int* stk = (FL & F_GROUPS) ? stk_lds + tid : nullptr;
     uint32_t n_gen = c0;  // next sample whose camera ray is to be generated
     uint32_t n_buf = 0, n_cur = 0;
-    bool buf = false, active = false;
+    bool buf = false, active = false, pending = false;
     PathState P;
+    Hit hp;
     for (;;) {
         if (!__any(active || buf || n_gen < c1)) break;
         const bool need = !buf && n_gen < c1;
@@ -805,23 +981,70 @@ __global__ __launch_bounds__(256, 4) void trace_kernel(DevScene S, uint32_t samp
         if (n_need >= kRefillNeed || n_starve >= kRefillStarve || (n_starve > 0 && !__any(active))) {
             if (need) {
                 d4 ro, rd;
-                ray_for_pixel<(FL & F_DOF) != 0>(S.cam, cc, sunf, (unsigned)px, (unsigned)py,
-                                                 noise3d(fgi, (float)n_gen, fgi2), noise3d(fgi, fgi2, (float)n_gen),
-                                                 (int)n_gen, ro, rd);
-                cam_ro[tid] = ro;
-                cam_rd[tid] = rd;
+                ray_for_pixel<(FL & F_DOF) != 0, A>(S.cam, cc, sunf, (unsigned)px, (unsigned)py,
+                                                    noise3d(fgi, (float)n_gen, fgi2), noise3d(fgi, fgi2, (float)n_gen),
+                                                    (int)n_gen, ro, rd);
+                cam_lds[0 * 256 + tid] = ro.x;
+                cam_lds[1 * 256 + tid] = ro.y;
+                cam_lds[2 * 256 + tid] = ro.z;
+                cam_lds[3 * 256 + tid] = rd.x;
+                cam_lds[4 * 256 + tid] = rd.y;
+                cam_lds[5 * 256 + tid] = rd.z;
+                if constexpr (!A) {
+                    cam_lds[6 * 256 + tid] = ro.w;
+                    cam_lds[7 * 256 + tid] = rd.w;
+                }
                 n_buf = n_gen;
                 n_gen++;
                 buf = true;
             }
         }
         if (!active && buf) {
-            start_path(P, cam_ro[tid], cam_rd[tid]);
+            const d4 cro = mk(cam_lds[0 * 256 + tid], cam_lds[1 * 256 + tid], cam_lds[2 * 256 + tid],
+                              A ? 1.0 : cam_lds[6 * 256 + tid]);
+            const d4 crd = mk(cam_lds[3 * 256 + tid], cam_lds[4 * 256 + tid], cam_lds[5 * 256 + tid],
+                              A ? 0.0 : cam_lds[7 * 256 + tid]);
+            start_path<A>(P, cro, crd);
             n_cur = n_buf;
             buf = false;
             active = true;
         }
-        if (active && bounce_step<FL>(S, stk, P, fgi, n_cur)) {
+        // Closest hit.  Scenes with BVH groups defer the walks: a lane whose ray
+        // needs one parks (pending, keeping its primitives' best in hp) and the
+        // wave walks all parked lanes together once kWalkBatch are parked or no
+        // lane is ready to shade -- a walk costs the whole wave its longest
+        // traversal, so it should run with many lanes, not the ~10 % of rays
+        // that reach a mesh in any one bounce.  Each lane still traces its
+        // samples in order, and the closest hit does not depend on when or in
+        // which order candidates are examined (lexicographic minimum, better()).
+        bool ready = false;
+        Hit h;
+        if (active && !pending) {
+            if (P.dead) {
+                h.obj = -1;
+                ready = true;
+            } else {
+                h = find_closest_prims<FL>(S, P.ro, P.rd);
+                if ((FL & F_GROUPS) && group_needs_walk<A>(S, P.ro, P.rd, h)) {
+                    pending = true;
+                    hp = h;
+                } else {
+                    ready = true;
+                }
+            }
+        }
+        if (FL & F_GROUPS) {
+            const int n_pend = __popcll(__ballot(pending));
+            if (n_pend >= kWalkBatch || (n_pend > 0 && !__any(ready))) {
+                if (pending) {
+                    h = hp;
+                    group_walks<A>(S, stk, P.ro, P.rd, h);
+                    pending = false;
+                    ready = true;
+                }
+            }
+        }
+        if (ready && bounce_shade<FL>(S, P, h, fgi, n_cur)) {
             cr = cr + P.ar;  // colors += accumColor (tracer.cl:1179)
             cg = cg + P.ag;
             cb = cb + P.ab;
@@ -921,6 +1144,7 @@ __global__ __launch_bounds__(256) void seeds_kernel(double* __restrict__ seeds, 
 
 // ---- host-side launch wrappers (called from ptmi_api.cpp) ----------------------
 const void* trace_kernel_symbol(int flags) {
+    if (flags & F_PROJ) return reinterpret_cast<const void*>(&trace_kernel<F_ALL | F_PROJ>);
     switch (flags & F_ALL) {
 #define K(f) \
     case f: return reinterpret_cast<const void*>(&trace_kernel<f>);
@@ -935,6 +1159,11 @@ hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, uint32_t
                         const double* seeds, const double* sunf, double* out, hipStream_t st) {
     const int tiles = ((S.cam.width + kTile - 1) / kTile) * ((S.cam.height + kTile - 1) / kTile);
     dim3 grid((tiles + kWavesPerBlock - 1) / kWavesPerBlock, nchunks);
+    if (flags & F_PROJ) {  // non-affine scene: one generic instantiation with the literal w arithmetic
+        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ>, grid, dim3(256), 0, st, S, samples, s_begin, s_end,
+                           chunk_len, tile_stride, tile_offset, seeds, sunf, out);
+        return hipGetLastError();
+    }
     switch (flags & F_ALL) {
 #define K(f)                                                                                                   \
     case f:                                                                                                    \
@@ -965,3 +1194,16 @@ hipError_t launch_seeds(double* seeds, uint32_t n, uint64_t stream, hipStream_t 
 }
 
 }  // namespace ptmi
+
+#if PTMI_STATS
+namespace ptmi {
+int stats_read(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi_stats), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(ptmi_stats), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+}  // namespace ptmi
+#endif

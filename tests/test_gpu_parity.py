@@ -64,15 +64,17 @@ def test_hip_matches_live_reference(scene, w, h, spp, ap, fl, seed):
     assert err < 1e-12, "%s: L-inf %.3e (expected rounding-level agreement)" % (scene, err)
 
 
-@pytest.mark.parametrize("scene,ap", [("reference", 0.0), ("default", 0.15), ("teapot", 0.0)])
-def test_generic_instantiation_matches(monkeypatch, scene, ap):
-    """The feature-specialised kernel instantiation and the generic one (all
-    features compiled in, PTMI_FORCE_FLAGS=15) give identical images."""
+@pytest.mark.parametrize("force", ["15", "31"])
+@pytest.mark.parametrize("scene,ap", [("reference", 0.0), ("default", 0.15), ("teapot", 0.0), ("gopher", 0.0)])
+def test_generic_instantiation_matches(monkeypatch, scene, ap, force):
+    """The feature-specialised kernel instantiation and the generic ones give
+    identical images: 15 = all features compiled in (affine), 31 = all features
+    with the literal double4 w-lane arithmetic (the path for non-affine scenes)."""
     w, h, spp = 40, 24, 3
     objs, tris, grps, cam = scene_inputs(scene, w, h, ap, 1.6 if ap else 0.0)
     seeds = layout.seeds_go_float64(w * h, 77)
     spec = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
-    monkeypatch.setenv("PTMI_FORCE_FLAGS", "15")
+    monkeypatch.setenv("PTMI_FORCE_FLAGS", force)
     gen = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
     assert np.array_equal(spec, gen)
 

@@ -1,0 +1,28 @@
+"""DIAGNOSTIC: traversal counters of the BVH path (libptmi_stats.so, PTMI_STATS).
+    PTMI_LIB=pathtracer-ocl_amd/build/libptmi_stats.so python tools/bvh_stats.py [scene] [spp]
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "pathtracer-ocl_amd")]
+import torch  # noqa: E402,F401
+from ptmi import api, layout  # noqa: E402
+from tests.scene_inputs import scene_inputs  # noqa: E402
+
+scene = sys.argv[1] if len(sys.argv) > 1 else "teapot"
+spp = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+W, H = 1280, 960
+lib = api.load_library()
+buf = (ctypes.c_ulonglong * 8)()
+lib.ptmi_stats_read(buf, 1)
+objs, tris, grps, cam = scene_inputs(scene, W, H)
+api.Trace(objs, tris, grps, 0, spp, cam, seeds=layout.seeds_go_float64(W * H, 3))
+lib.ptmi_stats_read(buf, 1)
+names = ["walks", "node4", "leaves", "tri_tests", "verifies", "chain_boxes", "obj_gate_pass", "group_obj_tests"]
+v = dict(zip(names, buf))
+n = W * H * spp
+print(scene, "spp", spp)
+for k in names:
+    print("  %-16s %14d  per sample %8.3f  per walk %8.3f" % (k, v[k], v[k] / n, v[k] / max(v["walks"], 1)))
