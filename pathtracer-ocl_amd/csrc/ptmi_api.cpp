@@ -226,19 +226,19 @@ int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, u
         std::memcpy(st[t].n3, b + 224, 32);
         std::memcpy(st[t].color, b + 256, 32);
     }
-    // Per distinct BVH root: the triangle traversal index (ptmi_bvh.cpp).
+    // Per group object: one traversal index over all its roots' triangles
+    // (ptmi_bvh.cpp); the object then refers to its RootRec (child_count 1).
     index = RootIndex{};
-    root_rec.assign(roots.size(), RootRec{});
-    std::vector<int32_t> built(n_grp, -1);  // roots shared by several objects are built once
-    for (size_t i = 0; i < roots.size(); i++) {
-        const int32_t r = roots[i];
-        if (built[r] < 0) {
-            const int rc = build_root_index(tris, nodes, tri_off, tri_cnt, r, index, &root_rec[i], err, err_len);
-            if (rc) return rc;
-            built[r] = (int32_t)i;
-        } else {
-            root_rec[i] = root_rec[built[r]];
-        }
+    root_rec.clear();
+    for (DevObject& o : objs) {
+        if (o.type != 4) continue;
+        RootRec rec;
+        const int rc = build_object_index(tris, nodes, tri_off, tri_cnt, roots.data() + o.child_base, o.child_count,
+                                          index, &rec, err, err_len);
+        if (rc) return rc;
+        o.child_base = (int32_t)root_rec.size();
+        o.child_count = 1;
+        root_rec.push_back(rec);
     }
     return PTMI_OK;
 }

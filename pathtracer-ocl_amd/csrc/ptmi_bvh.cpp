@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -64,7 +65,12 @@ void grow(double* mn, double* mx, const double* a, const double* b) {
 struct Builder {
     std::vector<Prim>& prims;
     std::vector<BNode> nodes;
-    explicit Builder(std::vector<Prim>& p) : prims(p) {}
+    double c_tri = 2.0;        // SAH cost of a triangle test relative to a node visit
+    int leaf_max = kLeafMax;   // triangles per leaf (<= kLeafMax)
+    explicit Builder(std::vector<Prim>& p) : prims(p) {
+        if (const char* e = std::getenv("PTMI_BVH_CTRI")) c_tri = std::atof(e);  // tuning experiments
+        if (const char* e = std::getenv("PTMI_BVH_LEAF")) leaf_max = std::max(1, std::min(kLeafMax, std::atoi(e)));
+    }
 
     int make_leaf(int lo, int hi, const double* mn, const double* mx) {
         BNode n;
@@ -88,13 +94,13 @@ struct Builder {
         // Depth budget: when the remaining levels barely suffice for a balanced
         // tree, split at the median (guarantees depth <= kMaxBinaryDepth).
         int need = 0;
-        while ((kLeafMax << need) < n) need++;
+        while ((leaf_max << need) < n) need++;
         int axis = 0;
         for (int k = 1; k < 3; k++)
             if (cmx[k] - cmn[k] > cmx[axis] - cmn[axis]) axis = k;
         int mid = -1;
         if (need + 1 >= kMaxBinaryDepth - depth || cmx[axis] - cmn[axis] <= 0.0) {
-            if (n <= kLeafMax) return make_leaf(lo, hi, mn, mx);
+            if (n <= leaf_max) return make_leaf(lo, hi, mn, mx);
             mid = (lo + hi) / 2;
             std::nth_element(prims.begin() + lo, prims.begin() + mid, prims.begin() + hi,
                              [axis](const Prim& a, const Prim& b) {
@@ -141,8 +147,10 @@ struct Builder {
                     }
                 }
             }
-            const double leaf_cost = area(mn, mx) * n;
-            if (n <= kLeafMax && (best_axis < 0 || leaf_cost <= 1.2 * best + area(mn, mx)))
+            // SAH: a node visit costs 1 (four FP32 slab tests), a triangle test
+            // c_tri (FP64 Moller-Trumbore), in units of the parent's area.
+            const double leaf_cost = area(mn, mx) * n * c_tri;
+            if (n <= leaf_max && (best_axis < 0 || leaf_cost <= area(mn, mx) + c_tri * best))
                 return make_leaf(lo, hi, mn, mx);
             if (best_axis < 0) {
                 mid = (lo + hi) / 2;
@@ -179,15 +187,19 @@ int32_t leaf_code(int32_t first, int32_t count) { return -((first << 3) | count)
 
 }  // namespace
 
-int build_root_index(const uint8_t* tris, const std::vector<DevNode>& nodes, const std::vector<int32_t>& tri_off,
-                     const std::vector<int32_t>& tri_cnt, int32_t root, RootIndex& out, RootRec* rec, char* err,
-                     size_t err_len) {
+int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, const std::vector<int32_t>& tri_off,
+                       const std::vector<int32_t>& tri_cnt, const int32_t* roots, int n_roots, RootIndex& out,
+                       RootRec* rec, char* err, size_t err_len) {
     *rec = RootRec{};
     int32_t* entry = &rec->entry;
-    // Reference subtree of `root` (children > 0 are present, tracer.cl:683/704)
-    // with each node's gate chain relative to the root.
+    const int32_t root = n_roots > 0 ? roots[0] : -1;  // for messages
+    // Reference subtrees of the object's roots (children > 0 are present,
+    // tracer.cl:683/704), each node with its gate chain: the path from its root.
+    // A triangle reachable from two roots appears twice, each with its own chain
+    // (the reference tests it once per root walk).
     std::vector<Prim> prims;
-    std::vector<std::pair<int32_t, std::vector<int32_t>>> todo{{root, {root}}};
+    std::vector<std::pair<int32_t, std::vector<int32_t>>> todo;
+    for (int i = n_roots - 1; i >= 0; i--) todo.push_back({roots[i], {roots[i]}});
     while (!todo.empty()) {
         auto [g, path] = todo.back();
         todo.pop_back();

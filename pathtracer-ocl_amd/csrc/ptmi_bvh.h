@@ -15,11 +15,12 @@ struct RootIndex {  // appended to by every root built into one scene
     std::vector<ChainBox> chain_boxes;
 };
 
-// Build the index of the triangles below reference node `root` (its subtree in
-// `nodes`, triangle ranges tri_off/tri_cnt) into `out`; *entry receives the
-// root record (entry code + widened hull).  Returns PTMI_OK or an error.
-int build_root_index(const uint8_t* tris, const std::vector<DevNode>& nodes, const std::vector<int32_t>& tri_off,
-                     const std::vector<int32_t>& tri_cnt, int32_t root, RootIndex& out, RootRec* rec, char* err,
-                     size_t err_len);
+// Build the traversal index of all triangles below the reference roots
+// roots[0..n_roots) of one group object (their subtrees in `nodes`, triangle
+// ranges tri_off/tri_cnt) into `out`; *rec receives the entry code and the
+// widened hull.  Returns PTMI_OK or an error.
+int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, const std::vector<int32_t>& tri_off,
+                       const std::vector<int32_t>& tri_cnt, const int32_t* roots, int n_roots, RootIndex& out,
+                       RootRec* rec, char* err, size_t err_len);
 
 }  // namespace ptmi
