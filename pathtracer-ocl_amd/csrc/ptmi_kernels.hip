@@ -361,7 +361,10 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 
         const int c = T.chain;
         if (c != vchain) {
 #if !(defined(PTMI_EXP) && (PTMI_EXP & 8))
-            if (!verify_chain(S, c, o, d)) return;
+            if (!verify_chain(S, c, o, d)) {
+                PTMI_COUNT(5);  // (stats build: gate rejections; chain box count is not tallied)
+                return;
+            }
 #endif
             vchain = c;
         }
@@ -385,7 +388,6 @@ __device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o,
     const int len = chain & 31;
     PTMI_COUNT(4);
     for (int i = 0; i < len; i++) {
-        PTMI_COUNT(5);
         double a, b;
         if (!ray_box_ref(o, d, r, B[i].mn, B[i].mx, a, b)) return false;
     }

@@ -1,0 +1,77 @@
+"""Adversarial BVH meshes for the parity tests (synthetic OBJ text fed through
+ptmi's restatement of the Go scene pipeline: ParseObj, ComputeVertexNormals,
+Divide(50), BuildCLGroup -- scenes.teapot_scene with obj_path).
+
+They target the exactness arguments of the BVH path:
+  * "flat"   -- a planar grid (z = 0): every reference node box has zero
+                thickness, so the reference's line-box test (tmin < tmax) fails
+                whenever the z slab binds; ptmi's own index finds those hits
+                and must drop them through the exact gate check;
+  * "stairs" -- axis-aligned faces sharing edges and vertices: rays through
+                shared edges, boxes touching faces exactly;
+  * "dupes"  -- every triangle listed twice: exact t ties between different
+                triangle indices (tie-break by index, both gated).
+"""
+import os
+import tempfile
+
+from ptmi import layout, scenes
+
+
+def _grid(nx, ny, x0, y0, s, z, faces, verts, flip=False):
+    base = len(verts)
+    for j in range(ny + 1):
+        for i in range(nx + 1):
+            verts.append((x0 + i * s, y0 + j * s, z))
+    for j in range(ny):
+        for i in range(nx):
+            a = base + j * (nx + 1) + i + 1
+            b, c, d = a + 1, a + nx + 1, a + nx + 2
+            faces += [(a, b, d), (a, d, c)] if not flip else [(a, d, b), (a, c, d)]
+
+
+def obj_text(kind):
+    verts, faces = [], []
+    if kind == "flat":
+        _grid(24, 24, -6.0, -1.0, 0.5, 0.0, faces, verts)
+    elif kind == "stairs":
+        for k in range(8):  # step k: top (y = k/2 + 1/2) and riser (z = -k/2) faces, 4x4 quads each
+            y, z = 0.5 * k, -0.5 * k
+            base = len(verts)
+            for j in range(5):
+                for i in range(5):
+                    verts.append((-4.0 + 2.0 * i, y + 0.5, z - 0.125 * j))  # tread
+            for j in range(4):
+                for i in range(4):
+                    a = base + j * 5 + i + 1
+                    faces += [(a, a + 1, a + 6), (a, a + 6, a + 5)]
+            base = len(verts)
+            for j in range(5):
+                for i in range(5):
+                    verts.append((-4.0 + 2.0 * i, y + 0.125 * j, z))  # riser
+            for j in range(4):
+                for i in range(4):
+                    a = base + j * 5 + i + 1
+                    faces += [(a, a + 1, a + 6), (a, a + 6, a + 5)]
+    elif kind == "dupes":
+        _grid(12, 12, -6.0, -1.0, 1.0, 0.0, faces, verts)
+        _grid(12, 12, -6.0, -1.0, 1.0, -2.0, faces, verts, flip=True)
+        faces = faces + list(faces)  # every triangle twice
+    else:
+        raise ValueError(kind)
+    lines = ["v %.17g %.17g %.17g" % v for v in verts]
+    lines += ["g mesh"]
+    lines += ["f %d %d %d" % f for f in faces]
+    return "\n".join(lines) + "\n", len(faces)
+
+
+def scene_inputs(kind, width, height, aperture=0.0, focal_length=0.0):
+    """-> (objects, triangles, groups, camera) records of the adversarial scene."""
+    text, _ = obj_text(kind)
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "%s.obj" % kind)
+        with open(p, "w") as f:
+            f.write(text)
+        sc = scenes.teapot_scene(width, height, aperture, focal_length, obj_path=p)
+    objs, tris, grps = layout.build_scene_buffer_cl(sc.objects)
+    return objs, tris, grps, layout.camera_record(sc.camera)

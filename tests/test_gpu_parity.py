@@ -156,3 +156,21 @@ def test_errors_are_loud():
     # device index < 0 selects device 0 (ocltracer.go:138-140)
     out = api.Trace(objs, tris, grps, -1, 1, cam, seed_stream=1)
     assert out.shape == (8 * 8 * 4,)
+
+
+@pytest.mark.parametrize("kind", ["flat", "stairs", "dupes"])
+@pytest.mark.parametrize("ap", [0.0, 0.15])
+def test_hip_matches_live_reference_adversarial_bvh(kind, ap):
+    """Meshes built to break the BVH exactness arguments (tests/adversarial.py):
+    zero-thickness reference boxes, shared edges, exact t ties."""
+    if not pyoracle.ref_available():
+        pytest.skip("oracle/_ref not built")
+    from tests import adversarial
+    w, h, spp = 96, 64, 4
+    objs, tris, grps, cam = adversarial.scene_inputs(kind, w, h, ap, 1.6 if ap else 0.0)
+    seeds = layout.seeds_go_float64(w * h, 300 + len(tris))
+    t2, g2 = layout.pad_empty(tris, grps)
+    ref = pyoracle.ref_trace(objs, t2, g2, cam, spp, seeds)
+    out = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    err = np.abs(out - ref).max()
+    assert err < 1e-12, "%s: L-inf %.3e vs live reference" % (kind, err)

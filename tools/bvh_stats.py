@@ -12,6 +12,9 @@ from ptmi import api, layout  # noqa: E402
 from tests.scene_inputs import scene_inputs  # noqa: E402
 
 scene = sys.argv[1] if len(sys.argv) > 1 else "teapot"
+if scene.startswith("adv:"):
+    from tests import adversarial
+    scene_inputs = lambda n, w, h: adversarial.scene_inputs(n[4:], w, h)  # noqa: E731
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 W, H = 1280, 960
 lib = api.load_library()
@@ -20,7 +23,7 @@ lib.ptmi_stats_read(buf, 1)
 objs, tris, grps, cam = scene_inputs(scene, W, H)
 api.Trace(objs, tris, grps, 0, spp, cam, seeds=layout.seeds_go_float64(W * H, 3))
 lib.ptmi_stats_read(buf, 1)
-names = ["walks", "node4", "leaves", "tri_tests", "verifies", "chain_boxes", "obj_gate_pass", "group_obj_tests"]
+names = ["walks", "node4", "leaves", "tri_tests", "verifies", "gate_rejects", "obj_gate_pass", "group_obj_tests"]
 v = dict(zip(names, buf))
 n = W * H * spp
 print(scene, "spp", spp)
