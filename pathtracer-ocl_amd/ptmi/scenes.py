@@ -18,6 +18,7 @@ from .gomath import Tan
 PI_OVER_2 = 1.5707963267948966    # float64(math.Pi / 2)
 PI_OVER_3 = 1.0471975511965979    # float64(math.Pi / 3)  (!= math.pi / 3)
 PI_OVER_4 = 0.7853981633974483    # float64(math.Pi / 4)
+PI_OVER_12 = 0.26179938779914946  # float64(math.Pi / 12)  (Go: exact constant, then rounded; != math.pi / 12)
 
 # The OBJ/MTL assets are read from the reference checkout (this container only);
 # the GPU box uses the scene records pre-built from them (tests/golden/scene_*.npz,
@@ -240,8 +241,125 @@ def gopher_scene(width, height, aperture=0.0, focal_length=0.0):
     return Scene(cam, objects)
 
 
+def _light_sphere(emission, color=None):
+    """The flattened ceiling light sphere of the Cornell scenes (translate (0,.399,0),
+    scale (0.283, 0.01, 0.283)) with a LightBulb material."""
+    src = shapes.Sphere()
+    src.set_transform(geom.translate(0, .399, 0))
+    src.set_transform(geom.scale(0.283, 0.01, 0.283))
+    light = shapes.new_light_bulb()
+    light.emission = emission
+    if color is not None:
+        light.color = color
+    src.set_material(light)
+    return src
+
+
+def _sphere(t, s, material):
+    sp = shapes.Sphere()
+    sp.set_transform(geom.translate(*t))
+    sp.set_transform(geom.scale(s, s, s))
+    sp.set_material(material)
+    return sp
+
+
+def reflection_scene(width, height, aperture=0.0, focal_length=0.0):
+    """ReflectionsScene (scenes/reflections.go:12-83): mirror + diffuse sphere."""
+    cam = _std_camera(width, height, aperture, focal_length)
+    left, right, floor, ceil, back, _front = _walls(.4)
+    lsp = _sphere((-0.35, -0.28, -0.15), 0.12, shapes.new_mirror())
+    rsp = _sphere((0, -0.24, -0.30), 0.16, shapes.new_diffuse(0.9, 0.8, 0.7))
+    light = _light_sphere(geom.color(9, 9, 9))
+    return Scene(cam, [light, floor, ceil, left, right, back, lsp, rsp])
+
+
+def _transparency_spheres(left_t, left_s, right_t, right_s):
+    """Glass (RI 1.52, reflectivity 0.05), diffuse with RI 1.57, mirror
+    (scenes/transparency*.go:62-82)."""
+    lsp = _sphere(left_t, left_s, shapes.new_glass())
+    mmat = shapes.new_diffuse(0.9, 0.8, 0.7)
+    msp = _sphere((0, -0.24, -0.30), 0.16, mmat)
+    msp.material.refractive_index = 1.57
+    rsp = _sphere(right_t, right_s, shapes.new_mirror())
+    return lsp, msp, rsp
+
+
+def transparency_scene(width, height, aperture=0.0, focal_length=0.0):
+    """TransparencyScene (scenes/transparency.go:13-101)."""
+    cam = _std_camera(width, height, aperture, focal_length)
+    left, right, floor, ceil, back, _front = _walls(.6)
+    lsp, msp, rsp = _transparency_spheres((-0.25, -0.28, 0.25), 0.12, (0.25, -0.28, 0.25), 0.12)
+    light = _light_sphere(geom.color(9, 9, 9), geom.color(1, 1, 1))
+    return Scene(cam, [light, floor, ceil, left, right, back, lsp, msp, rsp])
+
+
+def _cube_light(t, s, emission):
+    c = shapes.Cube()
+    c.set_transform(geom.translate(*t))
+    c.set_transform(geom.scale(*s))
+    m = shapes.new_light_bulb()
+    m.emission = emission
+    m.color = geom.color(1, 1, 1)
+    c.set_material(m)
+    return c
+
+
+def transparency_f_light_scene(width, height, aperture=0.0, focal_length=0.0):
+    """TransparencyFLightScene (scenes/transparency_f_light.go:13-113): three cube
+    lights forming an F."""
+    cam = _std_camera(width, height, aperture, focal_length)
+    left, right, floor, ceil, back, _front = _walls(.6)
+    lsp, msp, rsp = _transparency_spheres((-0.25, -0.18, 0.25), 0.14, (0.35, -0.23, 0.2), 0.17)
+    e = geom.color(9, 9, 9)
+    l1 = _cube_light((-0.125, .3999, 0.05), (0.05, 0.01, 0.45), e)
+    l2 = _cube_light((-0.02, .3999, -0.35), (0.075, 0.01, 0.05), e)
+    l3 = _cube_light((-0.05, .3999, 0), (0.075, 0.01, 0.05), e)
+    return Scene(cam, [floor, ceil, left, right, back, lsp, msp, rsp, l1, l2, l3])
+
+
+def transparency_quad_lights_scene(width, height, aperture=0.0, focal_length=0.0):
+    """TransparencyQuadLightsScene (scenes/transparency_quadlights.go:13-106)."""
+    cam = _std_camera(width, height, aperture, focal_length)
+    left, right, floor, ceil, back, _front = _walls(.6)
+    lsp, msp, rsp = _transparency_spheres((-0.25, -0.18, 0.25), 0.14, (0.35, -0.23, 0.2), 0.17)
+    lights = [_cube_light((-0.25 + float(i) * 0.5, .399, -0.25 + float(j) * 0.5), (0.15, 0.01, 0.15),
+                          geom.color(9, 9, 9)) for i in range(2) for j in range(2)]
+    return Scene(cam, [floor, ceil, left, right, back, lsp, msp, rsp] + lights)
+
+
+def transparent_teapot_scene(width, height, aperture=0.0, focal_length=0.0, obj_path=None):
+    """TransparentTeapotScene (scenes/transparent_teapot.go:14-128): a thin-glass
+    (refractive index -1, reflectivity 0.2) BVH teapot and a glass sphere."""
+    shapes.reset_subgroup_counter()
+    cam = _std_camera(width, height, aperture, focal_length)
+    left, right, floor, ceil, back, _front = _walls(.6)
+    lsp = _sphere((-0.25, -0.28, 0.25), 0.12, shapes.new_diffuse(0.9, 0.8, 0.7))
+    rsp = _sphere((0.25, -0.28, 0.25), 0.12, shapes.new_glass())
+    mtrl = shapes.new_glass()
+    mtrl.refractive_index = -1.0
+    mtrl.reflectivity = 0.2
+    model = _load_obj("teapot.obj") if obj_path is None else objparser.parse_obj(open(obj_path).read())
+    group = model.to_group()
+    tris = list(group.children[0].children)
+    objparser.compute_vertex_normals(tris)
+    group.bounds()
+    group.set_transform(geom.translate(0, -0.38, -0.2))
+    group.set_transform(geom.rotate_y(PI_OVER_12))
+    group.set_transform(geom.scale(0.1, 0.1, 0.1))
+    group.set_material(mtrl)
+    shapes.divide(group, 50)
+    group.bounds()
+    light = _light_sphere(geom.color(9, 9, 9))
+    return Scene(cam, [light, floor, ceil, left, right, back, lsp, rsp, group])
+
+
 SCENES = {
     "reference": reference_scene,
+    "reflection": reflection_scene,
+    "transparency": transparency_scene,
+    "transparency_f_light": transparency_f_light_scene,
+    "transparency_quad_lights": transparency_quad_lights_scene,
+    "transparent_teapot": transparent_teapot_scene,
     "teapot": teapot_scene,
     "gopher": gopher_scene,
     "default": ocl_scene,

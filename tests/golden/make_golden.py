@@ -35,6 +35,12 @@ CASES = {
     "teapot_32x24_s4": ("teapot", 32, 24, 4, 0.0, 0.0, 17),
     "gopher_32x24_s4": ("gopher", 32, 24, 4, 0.0, 0.0, 18),
     "ref_160x120_s4": ("reference", 160, 120, 4, 0.0, 0.0, 19),
+    # material paths: glass (RI 1.52) / diffuse RI 1.57 / mirror / thin glass (RI -1)
+    "transp_48x32_s6": ("transparency", 48, 32, 6, 0.0, 0.0, 20),
+    "transp_quad_48x32_s4": ("transparency_quad_lights", 48, 32, 4, 0.0, 0.0, 21),
+    "transp_f_dof_48x32_s5": ("transparency_f_light", 48, 32, 5, 0.15, 1.6, 22),
+    "reflect_48x32_s6": ("reflection", 48, 32, 6, 0.0, 0.0, 23),
+    "glassteapot_32x24_s4": ("transparent_teapot", 32, 24, 4, 0.0, 0.0, 24),
 }
 
 

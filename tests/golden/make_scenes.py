@@ -1,6 +1,6 @@
 """Generate the committed BVH scene records (inputs, not reference code).
 
-The teapot / gopher scenes are built by ptmi's restatement of the reference's OBJ
+The teapot / gopher / transparent_teapot scenes are built by ptmi's restatement of the reference's OBJ
 parser + BVH build from the OBJ assets in the reference checkout
 (/root/reference/assets, this container only).  The resulting kernel input
 records (CLObject / CLTriangle / CLGroup bytes, layout.py) are saved so tests and
@@ -21,7 +21,7 @@ from ptmi import layout, scenes  # noqa: E402
 
 
 def main():
-    for name in ("teapot", "gopher"):
+    for name in ("teapot", "gopher", "transparent_teapot"):
         sc = scenes.SCENES[name](64, 48)
         objs, tris, grps = layout.build_scene_buffer_cl(sc.objects)
         out = os.path.join(HERE, "scene_%s.npz" % name)

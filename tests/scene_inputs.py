@@ -1,7 +1,7 @@
 """Kernel input records for the benchmark / parity scenes.
 
-``reference`` and ``default`` (OCLScene) are built on the fly by ptmi's scene
-restatement.  ``teapot`` / ``gopher`` load the records pre-built from the OBJ
+Scenes without meshes are built on the fly by ptmi's scene restatement.
+``teapot`` / ``gopher`` / ``transparent_teapot`` load the records pre-built from the OBJ
 assets (tests/golden/scene_*.npz, tests/golden/make_scenes.py) because the assets
 live in the reference checkout, which the GPU box does not have; only the camera
 record (a function of W/H/aperture/focal) is rebuilt.
@@ -16,6 +16,7 @@ sys.path.insert(0, os.path.join(HERE, "..", "pathtracer-ocl_amd"))
 from ptmi import layout, scenes  # noqa: E402
 
 _cache = {}
+MESH_SCENES = ("teapot", "gopher", "transparent_teapot")  # records from tests/golden/scene_<name>.npz
 
 
 def _load_mesh_scene(name):
@@ -29,7 +30,7 @@ def _load_mesh_scene(name):
 
 def scene_inputs(name, width, height, aperture=0.0, focal_length=0.0):
     """-> (objects, triangles, groups, camera) records (triangles/groups may be empty)."""
-    if name in ("teapot", "gopher"):
+    if name in MESH_SCENES:
         objs, tris, grps = _load_mesh_scene(name)
         cam = scenes._std_camera(width, height, aperture, focal_length)
         return objs, tris, grps, layout.camera_record(cam)

@@ -25,9 +25,12 @@ def _render(scene, w, h, spp, seeds, ap=0.0, fl=0.0):
     return api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
 
 
-@pytest.mark.parametrize("name", ["ref_64x48_s4", "ref_64x48_s16", "ref_40x30_s3", "ref_dof_64x48_s8",
-                                  "ocl_64x48_s8", "ocl_dof_48x32_s5", "teapot_32x24_s4", "gopher_32x24_s4",
-                                  "ref_160x120_s4"])
+GOLDEN = ["ref_64x48_s4", "ref_64x48_s16", "ref_40x30_s3", "ref_dof_64x48_s8", "ocl_64x48_s8", "ocl_dof_48x32_s5",
+          "teapot_32x24_s4", "gopher_32x24_s4", "ref_160x120_s4", "transp_48x32_s6", "transp_quad_48x32_s4",
+          "transp_f_dof_48x32_s5", "reflect_48x32_s6", "glassteapot_32x24_s4"]
+
+
+@pytest.mark.parametrize("name", GOLDEN)
 def test_hip_matches_reference_golden(golden_cases, name):
     if name not in golden_cases:
         pytest.skip("golden %s not generated" % name)
@@ -50,6 +53,13 @@ def test_hip_matches_reference_golden(golden_cases, name):
     ("teapot", 128, 96, 4, 0.0, 0.0, 106),
     ("gopher", 128, 96, 3, 0.0, 0.0, 107),
     ("teapot", 96, 64, 3, 0.15, 1.6, 108),
+    ("reflection", 96, 64, 6, 0.0, 0.0, 109),
+    ("transparency", 96, 64, 6, 0.0, 0.0, 110),
+    ("transparency", 72, 48, 5, 0.15, 1.6, 111),
+    ("transparency_f_light", 96, 64, 4, 0.0, 0.0, 112),
+    ("transparency_quad_lights", 96, 64, 4, 0.0, 0.0, 113),
+    ("transparent_teapot", 96, 64, 4, 0.0, 0.0, 114),
+    ("transparent_teapot", 64, 48, 3, 0.15, 1.6, 115),
 ])
 def test_hip_matches_live_reference(scene, w, h, spp, ap, fl, seed):
     if not pyoracle.ref_available():
@@ -174,3 +184,20 @@ def test_hip_matches_live_reference_adversarial_bvh(kind, ap):
     out = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
     err = np.abs(out - ref).max()
     assert err < 1e-12, "%s: L-inf %.3e vs live reference" % (kind, err)
+
+
+@pytest.mark.parametrize("scene,ap", [("transparency", 0.0), ("transparency_quad_lights", 0.15),
+                                      ("reflection", 0.0), ("transparent_teapot", 0.0)])
+def test_cpu_oracle_matches_live_reference_materials(scene, ap):
+    """The CPU oracle's material paths (refraction, thin glass, mirrors) against
+    the reference kernel itself -- the goldens pin the rest of the oracle."""
+    if not pyoracle.ref_available():
+        pytest.skip("oracle/_ref not built")
+    w, h, spp = 32, 24, 3
+    objs, tris, grps, cam = scene_inputs(scene, w, h, ap, 1.6 if ap else 0.0)
+    seeds = layout.seeds_go_float64(w * h, 500)
+    t2, g2 = layout.pad_empty(tris, grps)
+    ref = pyoracle.ref_trace(objs, t2, g2, cam, spp, seeds)
+    ora = pyoracle.cpu_trace(objs, t2, g2, cam, spp, seeds)
+    assert np.abs(ora - ref).max() < 1e-12
+

@@ -31,7 +31,8 @@ def test_golden_inputs_match_scene_restatement(golden_cases):
 
 @pytest.mark.parametrize("name", ["ref_64x48_s4", "ref_dof_64x48_s8", "ocl_64x48_s8", "teapot_32x24_s4",
                                   "ref_64x48_s16", "ref_40x30_s3", "ocl_dof_48x32_s5", "gopher_32x24_s4",
-                                  "ref_160x120_s4"])
+                                  "ref_160x120_s4", "transp_48x32_s6", "transp_quad_48x32_s4",
+                                  "transp_f_dof_48x32_s5", "reflect_48x32_s6", "glassteapot_32x24_s4"])
 def test_oracle_matches_reference_kernel(golden_cases, name):
     if name not in golden_cases:
         pytest.skip("golden %s not generated yet" % name)
