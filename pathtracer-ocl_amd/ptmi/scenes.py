@@ -241,6 +241,16 @@ def gopher_scene(width, height, aperture=0.0, focal_length=0.0):
     return Scene(cam, objects)
 
 
+def _labelled(objs, labels):
+    """Shape labels as the Go scene sets them (copied into CLObject.Label, scene.go:18-22)."""
+    for o, lbl in zip(objs, labels):
+        o.label = lbl
+    return objs
+
+
+_WALL_LABELS = ("leftwall", "rghtwall", "floor   ", "ceiling ", "backwall", "frntwall")
+
+
 def _light_sphere(emission, color=None):
     """The flattened ceiling light sphere of the Cornell scenes (translate (0,.399,0),
     scale (0.283, 0.01, 0.283)) with a LightBulb material."""
@@ -287,9 +297,11 @@ def _transparency_spheres(left_t, left_s, right_t, right_s):
 def transparency_scene(width, height, aperture=0.0, focal_length=0.0):
     """TransparencyScene (scenes/transparency.go:13-101)."""
     cam = _std_camera(width, height, aperture, focal_length)
-    left, right, floor, ceil, back, _front = _walls(.6)
-    lsp, msp, rsp = _transparency_spheres((-0.25, -0.28, 0.25), 0.12, (0.25, -0.28, 0.25), 0.12)
+    left, right, floor, ceil, back, _front = _labelled(_walls(.6), _WALL_LABELS)
+    lsp, msp, rsp = _labelled(_transparency_spheres((-0.25, -0.28, 0.25), 0.12, (0.25, -0.28, 0.25), 0.12),
+                              ("left_spr", "mddl_spr", "right_spr"))
     light = _light_sphere(geom.color(9, 9, 9), geom.color(1, 1, 1))
+    light.label = "light   "
     return Scene(cam, [light, floor, ceil, left, right, back, lsp, msp, rsp])
 
 
@@ -308,22 +320,26 @@ def transparency_f_light_scene(width, height, aperture=0.0, focal_length=0.0):
     """TransparencyFLightScene (scenes/transparency_f_light.go:13-113): three cube
     lights forming an F."""
     cam = _std_camera(width, height, aperture, focal_length)
-    left, right, floor, ceil, back, _front = _walls(.6)
-    lsp, msp, rsp = _transparency_spheres((-0.25, -0.18, 0.25), 0.14, (0.35, -0.23, 0.2), 0.17)
+    left, right, floor, ceil, back, _front = _labelled(_walls(.6), _WALL_LABELS)
+    lsp, msp, rsp = _labelled(_transparency_spheres((-0.25, -0.18, 0.25), 0.14, (0.35, -0.23, 0.2), 0.17),
+                              ("left_spr", "mddl_spr", "right_spr"))
     e = geom.color(9, 9, 9)
     l1 = _cube_light((-0.125, .3999, 0.05), (0.05, 0.01, 0.45), e)
     l2 = _cube_light((-0.02, .3999, -0.35), (0.075, 0.01, 0.05), e)
     l3 = _cube_light((-0.05, .3999, 0), (0.075, 0.01, 0.05), e)
+    _labelled((l1, l2, l3), ("light 1", "light top", "light middle"))
     return Scene(cam, [floor, ceil, left, right, back, lsp, msp, rsp, l1, l2, l3])
 
 
 def transparency_quad_lights_scene(width, height, aperture=0.0, focal_length=0.0):
     """TransparencyQuadLightsScene (scenes/transparency_quadlights.go:13-106)."""
     cam = _std_camera(width, height, aperture, focal_length)
-    left, right, floor, ceil, back, _front = _walls(.6)
-    lsp, msp, rsp = _transparency_spheres((-0.25, -0.18, 0.25), 0.14, (0.35, -0.23, 0.2), 0.17)
+    left, right, floor, ceil, back, _front = _labelled(_walls(.6), _WALL_LABELS)
+    lsp, msp, rsp = _labelled(_transparency_spheres((-0.25, -0.18, 0.25), 0.14, (0.35, -0.23, 0.2), 0.17),
+                              ("left_spr", "mddl_spr", "right_spr"))
     lights = [_cube_light((-0.25 + float(i) * 0.5, .399, -0.25 + float(j) * 0.5), (0.15, 0.01, 0.15),
                           geom.color(9, 9, 9)) for i in range(2) for j in range(2)]
+    _labelled(lights, ["light %d-%d" % (i, j) for i in range(2) for j in range(2)])
     return Scene(cam, [floor, ceil, left, right, back, lsp, msp, rsp] + lights)
 
 
@@ -332,9 +348,10 @@ def transparent_teapot_scene(width, height, aperture=0.0, focal_length=0.0, obj_
     (refractive index -1, reflectivity 0.2) BVH teapot and a glass sphere."""
     shapes.reset_subgroup_counter()
     cam = _std_camera(width, height, aperture, focal_length)
-    left, right, floor, ceil, back, _front = _walls(.6)
+    left, right, floor, ceil, back, _front = _labelled(_walls(.6), _WALL_LABELS)
     lsp = _sphere((-0.25, -0.28, 0.25), 0.12, shapes.new_diffuse(0.9, 0.8, 0.7))
     rsp = _sphere((0.25, -0.28, 0.25), 0.12, shapes.new_glass())
+    _labelled((lsp, rsp), ("left_spr", "right_spr"))
     mtrl = shapes.new_glass()
     mtrl.refractive_index = -1.0
     mtrl.reflectivity = 0.2
@@ -349,7 +366,9 @@ def transparent_teapot_scene(width, height, aperture=0.0, focal_length=0.0, obj_
     group.set_material(mtrl)
     shapes.divide(group, 50)
     group.bounds()
+    group.label = "teapot  "
     light = _light_sphere(geom.color(9, 9, 9))
+    light.label = "light   "
     return Scene(cam, [light, floor, ceil, left, right, back, lsp, rsp, group])
 
 

@@ -47,6 +47,20 @@ def test_library_loads_and_identifies_gfx950():
     assert b"amdgcn-amd-amdhsa--gfx950" in blob  # the embedded code object targets gfx950
 
 
+def test_host_library_exports_every_declared_symbol():
+    """include/ptmi_host.h <-> libptmi_host.so (the native scene side + writers)."""
+    host_h = os.path.join(ROOT, "include", "ptmi_host.h")
+    lib = os.path.join(ROOT, "pathtracer-ocl_amd", "build", "libptmi_host.so")
+    if not os.path.exists(lib):
+        pytest.fail("libptmi_host.so not built")
+    src = re.sub(r"/\*.*?\*/", "", open(host_h).read(), flags=re.S)
+    declared = sorted(set(re.findall(r"\b(ptmi_host_[a-z_]+)\s*\(", src)))
+    assert len(declared) >= 5
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    assert not [s for s in declared if s not in exported]
+
+
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(FileNotFoundError):
         api.load_library(str(tmp_path / "libptmi.so"))
