@@ -1,0 +1,56 @@
+"""Summarise a tools/profile_round.sh output directory into profiles/<round>/:
+kernel_stats_<cfg>.csv, bench_<cfg>.json, pmc_c2*.{csv,json} and SUMMARY.md.
+    python tools/profile_summary.py gpurun_out/prof_r1b profiles/r1
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+CMDS = {"c2": "python3 bench.py --config c2 --steps 2 --warmup 1",
+        "c4": "python3 bench.py --config c4 --samples 256 --steps 1 --warmup 1 --no-cpu-baseline",
+        "c5": "python3 bench.py --config c5 --samples 256 --steps 1 --warmup 1 --no-cpu-baseline"}
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    lines = ["# rocprofv3 --kernel-trace --stats summaries (tools/profile_round.sh, one MI355X)", ""]
+    for c, cmd in CMDS.items():
+        shutil.copy(os.path.join(src, c, "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats_%s.csv" % c))
+        shutil.copy(os.path.join(src, "bench_%s.json" % c), os.path.join(dst, "bench_%s.json" % c))
+        lines.append("## %s: `%s`" % (c, cmd))
+        with open(os.path.join(dst, "kernel_stats_%s.csv" % c)) as f:
+            for r in csv.DictReader(f):
+                if "ptmi" not in r["Name"]:
+                    continue
+                name = r["Name"].split("(")[0].replace("void ", "")
+                lines.append("  %-36s calls %3s  avg %12.3f ms  total %12.3f ms" % (
+                    name, r["Calls"], float(r["AverageNs"]) / 1e6, float(r["TotalDurationNs"]) / 1e6))
+        with open(os.path.join(dst, "bench_%s.json" % c)) as f:
+            b = json.load(f)
+        rf = b["roofline"]
+        lines.append("  bench: value %.2f Msamples/s  kernel_ms_avg (HIP events) %.3f  achieved %.3f TF/s  frac %.4f"
+                     % (b["value"], rf["kernel_ms_avg"], rf["achieved"], rf["frac"]))
+        if b.get("cpu_baseline"):
+            cb = b["cpu_baseline"]
+            lines.append("  cpu_baseline: %.2f %s on %d cores (%s; %s)" % (cb["value"], cb["unit"], cb["cores"],
+                                                                         cb["kind"], cb["sample"]))
+        lines.append("")
+    shutil.copy(os.path.join(src, "pmc_c2.json"), os.path.join(dst, "pmc_c2.json"))
+    for k in ("fetch", "write"):
+        shutil.copy(os.path.join(src, "c2_%s" % k, "run_counter_collection.csv"),
+                    os.path.join(dst, "pmc_c2_%s.csv" % k))
+    with open(os.path.join(dst, "pmc_c2.json")) as f:
+        p = json.load(f)
+    lines.append("## c2 HBM traffic (separate --pmc passes, 1 frame): FETCH_SIZE %.1f KB (x2 gfx950 correction), "
+                 "WRITE_SIZE %.1f KB -> %.1f MB per launch" % (p["fetch_size_kb_raw_per_launch"],
+                                                             p["write_size_kb_per_launch"],
+                                                             p["hbm_bytes_per_launch"] / 1e6))
+    with open(os.path.join(dst, "SUMMARY.md"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
