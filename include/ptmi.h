@@ -72,6 +72,25 @@ int ptmi_trace(const void* objects, uint32_t n_obj, const void* triangles, uint3
                const void* camera, const double* seeds, uint64_t seed_stream,
                const ptmi_textures* textures, double* out_rgba, char* err, size_t err_len);
 
+/*
+ * ptmi_trace_multi -- ptmi_trace over several GPUs of this process:
+ * one host thread per entry of devices[0..n_devices) (an index may repeat), each
+ * rendering its shard of the frame into its own partial sums:
+ *   split 0 (sample): device d renders samples [d*S/n, (d+1)*S/n) of every pixel
+ *                     (global sample indices, as ptmi_scene_render);
+ *   split 1 (tile)  : device d renders every sample of the 8x8 tiles t with
+ *                     t % n == d.
+ * The partial frames are summed on the host in device order (deterministic; the
+ * tile split is exact, the sample split differs from one device only by FP64
+ * summation order) and normalised as ptmi_finalize.  Same record / seed / error
+ * contract as ptmi_trace.  (The torch.distributed driver, bench.py, does the same
+ * with one process per GPU and an RCCL all-reduce.)
+ */
+int ptmi_trace_multi(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
+                     const void* groups, uint32_t n_grp, const int* devices, uint32_t n_devices, int split,
+                     uint32_t samples, const void* camera, const double* seeds, uint64_t seed_stream,
+                     const ptmi_textures* textures, double* out_rgba, char* err, size_t err_len);
+
 /* --list-devices (cmd/pt/main.go:98-112). */
 int ptmi_device_count(void);
 int ptmi_device_name(int device_index, char* buf, size_t len);

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ptmi.h"
@@ -591,6 +592,87 @@ int ptmi_trace(const void* objects, uint32_t n_obj, const void* triangles, uint3
 }
 
 }  // extern "C"
+
+
+extern "C" int ptmi_trace_multi(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri, const void* groups,
+                     uint32_t n_grp, const int* devices, uint32_t n_devices, int split, uint32_t samples,
+                     const void* camera, const double* seeds, uint64_t seed_stream, const ptmi_textures* textures,
+                     double* out_rgba, char* err, size_t err_len) {
+    if (textures) {
+        for (int k = 0; k < 3; k++)
+            if (textures->count[k]) {
+                set_err(err, err_len, "texture arrays are not supported by this build");
+                return PTMI_ERR_UNSUPPORTED;
+            }
+    }
+    if (!out_rgba || samples == 0 || !devices || n_devices == 0 || (split != 0 && split != 1) || !camera) {
+        set_err(err, err_len, "ptmi_trace_multi: bad arguments");
+        return PTMI_ERR_ARG;
+    }
+    const uint32_t W = (uint32_t)rd<int32_t>((const uint8_t*)camera + 0);
+    const uint32_t H = (uint32_t)rd<int32_t>((const uint8_t*)camera + 4);
+    const size_t npix = (size_t)W * H;
+    std::vector<std::vector<double>> part(n_devices);
+    std::vector<int> rcs(n_devices, PTMI_OK);
+    std::vector<std::string> msgs(n_devices);
+    auto shard = [&](uint32_t d) {
+        char e[512] = {0};
+        int& rc = rcs[d];
+        ptmi_scene* s = nullptr;
+        double *d_seeds = nullptr, *d_sums = nullptr;
+        hipStream_t st = nullptr;
+        rc = ptmi_scene_create(devices[d], objects, n_obj, triangles, n_tri, groups, n_grp, camera, &s, e, sizeof(e));
+        if (!rc && (s->width != W || s->height != H)) rc = PTMI_ERR_ARG;
+        if (!rc && (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+                    hipMalloc((void**)&d_seeds, npix * sizeof(double)) != hipSuccess ||
+                    hipMalloc((void**)&d_sums, npix * 4 * sizeof(double)) != hipSuccess)) {
+            rc = PTMI_ERR_HIP;
+            std::snprintf(e, sizeof(e), "device %d: allocation failed", devices[d]);
+        }
+        if (!rc) {
+            if (seeds) {
+                if (hipMemcpyAsync(d_seeds, seeds, npix * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess)
+                    rc = PTMI_ERR_HIP;
+            } else {
+                rc = ptmi_fill_seeds(d_seeds, (uint32_t)npix, seed_stream, st, e, sizeof(e));
+            }
+        }
+        if (!rc) {
+            const uint32_t s0 = split == 0 ? (uint32_t)((uint64_t)d * samples / n_devices) : 0;
+            const uint32_t s1 = split == 0 ? (uint32_t)((uint64_t)(d + 1) * samples / n_devices) : samples;
+            part[d].assign(npix * 4, 0.0);
+            if (s1 > s0)
+                rc = ptmi_scene_render(s, samples, s0, s1, split == 1 ? n_devices : 1, split == 1 ? d : 0, d_seeds,
+                                       d_sums, 0, st, e, sizeof(e));
+            if (!rc && s1 > s0 &&
+                (hipMemcpyAsync(part[d].data(), d_sums, npix * 4 * sizeof(double), hipMemcpyDeviceToHost, st) !=
+                     hipSuccess ||
+                 hipStreamSynchronize(st) != hipSuccess))
+                rc = PTMI_ERR_HIP;
+        }
+        if (st) (void)hipStreamDestroy(st);
+        if (d_seeds) (void)hipFree(d_seeds);
+        if (d_sums) (void)hipFree(d_sums);
+        if (s) ptmi_scene_destroy(s);
+        msgs[d] = e;
+    };
+    std::vector<std::thread> threads;
+    for (uint32_t d = 0; d < n_devices; d++) threads.emplace_back(shard, d);
+    for (auto& t : threads) t.join();
+    for (uint32_t d = 0; d < n_devices; d++)
+        if (rcs[d]) {
+            set_err(err, err_len, "device %d: %s", devices[d], msgs[d].empty() ? "render failed" : msgs[d].c_str());
+            return rcs[d];
+        }
+    // Sum in device order, then ptmi_finalize's arithmetic (tracer.cl:1184-1187).
+    const double w = 1.0 / samples;
+    for (size_t i = 0; i < npix * 4; i++) {
+        double acc = part[0][i];
+        for (uint32_t d = 1; d < n_devices; d++) acc = acc + part[d][i];
+        out_rgba[i] = (i % 4 == 3) ? 1.0 : acc * w;
+    }
+    return PTMI_OK;
+}
 
 #if PTMI_STATS
 namespace ptmi {

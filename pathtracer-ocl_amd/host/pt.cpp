@@ -7,7 +7,8 @@
 //   --width 640 --height 480 --samples 1 --aperture 0 --focal-length 0
 //   --scene gopher --device-index 0 --list-devices --list-scenes
 // plus: --assets DIR (OBJ/MTL directory, default ./assets as the reference reads
-// them), --out FILE.png, --raw FILE.raw (raw/writer.go format), --seed N
+// them), --out FILE.png, --raw FILE.raw (raw/writer.go format), --gpus N and
+// --split sample|tile (ptmi_trace_multi over devices 0..N-1), --seed N
 // (per-pixel seeds from a fixed stream; default: time-seeded like Go's
 // rand.Float64 per pixel, ocltracer.go:260-263).
 // An unknown --scene renders the OCL scene, as main.go:86-88 does.
@@ -27,7 +28,8 @@ namespace {
 struct Cfg {
     int width = 640, height = 480, samples = 1, device_index = 0;
     double aperture = 0.0, focal_length = 0.0;
-    std::string scene = "gopher", assets = "assets", out, raw;
+    std::string scene = "gopher", assets = "assets", out, raw, split = "sample";
+    int gpus = 1;
     bool list_devices = false, list_scenes = false, have_seed = false;
     uint64_t seed = 0;
 };
@@ -36,7 +38,8 @@ struct Cfg {
     std::fprintf(stderr,
                  "%s\nusage: pt [--width N] [--height N] [--samples N] [--aperture F] [--focal-length F]\n"
                  "          [--scene NAME] [--device-index N] [--list-devices] [--list-scenes]\n"
-                 "          [--assets DIR] [--out FILE.png] [--raw FILE.raw] [--seed N]\n",
+                 "          [--assets DIR] [--out FILE.png] [--raw FILE.raw] [--gpus N] [--split sample|tile]\n"
+                 "          [--seed N]\n",
                  msg);
     std::exit(2);
 }
@@ -69,10 +72,13 @@ Cfg parse(int argc, char** argv) {
         else if (a == "--assets") c.assets = val();
         else if (a == "--out") c.out = val();
         else if (a == "--raw") c.raw = val();
+        else if (a == "--gpus") c.gpus = std::atoi(val().c_str());
+        else if (a == "--split") c.split = val();
         else if (a == "--seed") c.seed = std::strtoull(val().c_str(), nullptr, 10), c.have_seed = true;
         else usage(("unknown flag " + a).c_str());
     }
     if (c.width <= 0 || c.height <= 0 || c.samples <= 0) usage("width, height and samples must be positive");
+    if (c.gpus <= 0 || (c.split != "sample" && c.split != "tile")) usage("--gpus must be >= 1, --split sample|tile");
     return c;
 }
 
@@ -119,8 +125,16 @@ int main(int argc, char** argv) {
     std::vector<double> out(n * 4);
     const uint64_t stream =
         c.have_seed ? c.seed : (uint64_t)std::chrono::system_clock::now().time_since_epoch().count();
-    rc = ptmi_trace(r.objects, r.n_obj, r.triangles, r.n_tri, r.groups, r.n_grp, c.device_index, (uint32_t)c.samples,
-                    r.camera, nullptr, stream, nullptr, out.data(), err, sizeof(err));
+    if (c.gpus == 1) {
+        rc = ptmi_trace(r.objects, r.n_obj, r.triangles, r.n_tri, r.groups, r.n_grp, c.device_index,
+                        (uint32_t)c.samples, r.camera, nullptr, stream, nullptr, out.data(), err, sizeof(err));
+    } else {
+        std::vector<int> devs(c.gpus);
+        for (int d = 0; d < c.gpus; d++) devs[d] = d;
+        rc = ptmi_trace_multi(r.objects, r.n_obj, r.triangles, r.n_tri, r.groups, r.n_grp, devs.data(),
+                              (uint32_t)c.gpus, c.split == "tile" ? 1 : 0, (uint32_t)c.samples, r.camera, nullptr,
+                              stream, nullptr, out.data(), err, sizeof(err));
+    }
     ptmi_host_free_records(&r);
     if (rc) {
         std::fprintf(stderr, "ptmi_trace failed (%d): %s\n", rc, err);  // the reference: logrus.Fatalf

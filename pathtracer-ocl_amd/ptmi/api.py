@@ -26,7 +26,7 @@ PTMI_OK, PTMI_ERR_ARG, PTMI_ERR_DEVICE, PTMI_ERR_HIP, PTMI_ERR_UNSUPPORTED, PTMI
 
 EXPORTS = ("ptmi_trace", "ptmi_device_count", "ptmi_device_name", "ptmi_scene_create", "ptmi_scene_destroy",
            "ptmi_scene_size", "ptmi_scene_render", "ptmi_finalize", "ptmi_fill_seeds", "ptmi_build_info",
-           "ptmi_scene_set_timing", "ptmi_scene_kernel_time")
+           "ptmi_scene_set_timing", "ptmi_scene_kernel_time", "ptmi_trace_multi")
 
 
 class PtmiError(RuntimeError):
@@ -52,6 +52,9 @@ def load_library(path=None):
     cp = ctypes.c_char_p
     lib.ptmi_trace.restype = i32
     lib.ptmi_trace.argtypes = [vp, u32, vp, u32, vp, u32, i32, u32, vp, vp, ctypes.c_uint64, vp, vp, cp, sz]
+    lib.ptmi_trace_multi.restype = i32
+    lib.ptmi_trace_multi.argtypes = [vp, u32, vp, u32, vp, u32, vp, u32, i32, u32, vp, vp, ctypes.c_uint64, vp, vp,
+                                     cp, sz]
     lib.ptmi_device_count.restype = i32
     lib.ptmi_device_count.argtypes = []
     lib.ptmi_device_name.restype = i32

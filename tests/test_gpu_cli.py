@@ -43,3 +43,13 @@ def test_cli_lists(tmp_path):
     assert r.returncode == 0 and "reference" in r.stdout.split()
     r = subprocess.run([PT, "--list-devices"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "Index: 0" in r.stdout
+
+
+def test_cli_multi_device_flags(tmp_path):
+    """--gpus / --split run ptmi_trace_multi (one GPU here: --gpus 1 only)."""
+    png = tmp_path / "m.png"
+    r = subprocess.run([PT, "--scene", "reference", "--width", "24", "--height", "16", "--samples", "3", "--gpus", "1",
+                        "--split", "tile", "--seed", "3", "--out", str(png)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert os.path.getsize(png) > 0
