@@ -27,7 +27,8 @@
 #define PTMI_STATS 0
 #endif
 #if PTMI_STATS
-__device__ unsigned long long ptmi_stats[8];  // walks, node4, leaves, tri tests, verifies, chain boxes, obj gate pass, rays
+__device__ unsigned long long ptmi_stats[12];  // [11]: eager re-walks  // walks, node4, leaves, tri tests, verifies, gate rejects, obj gate
+                                               // pass, group obj tests, walk phases, lanes in phases, loop iters
 #define PTMI_COUNT(i) atomicAdd(&ptmi_stats[i], 1ull)
 #else
 #define PTMI_COUNT(i) ((void)0)
@@ -121,7 +122,7 @@ __device__ __noinline__ d4 normalize3(double x, double y, double z) {
             d = fma(pz, pz, fma(py, py, px * px));
         }
     }
-    const double s = rsqrt(d);
+    const double s = (PTMI_ABLATE & 256) ? __builtin_amdgcn_rsq(d) : rsqrt(d);  // DIAGNOSTIC 256
     return mk(px * s, py * s, pz * s, 0.0);
 }
 template <bool A>
@@ -186,6 +187,7 @@ __device__ __forceinline__ float noise3d(float x, float y, float z) {
     float b = y * 179.233f;
     float c = z * 237.212f;
     float s = (a + b) + c;
+    if (PTMI_ABLATE & 32) s = s * 1e-6f;  // DIAGNOSTIC: small-argument sin path only
     float v = sinf(s) * 43758.5453f;
     float r = fminf(v - floorf(v), 0x1.fffffep-1f);
     return isnan(v) ? v : (isinf(v) ? 0.0f : r);
@@ -217,9 +219,10 @@ __device__ __forceinline__ bool ray_box(d4 o, d4 d, const double* mn, const doub
 
 struct Hit {
     double t;
-    int obj;  // slot in DevScene::objs (type-run order)
-    int key;  // the object's index in the reference's list
-    int tri;
+    int obj;    // slot in DevScene::objs (type-run order)
+    int key;    // the object's index in the reference's list
+    int tri;    // reference triangle index, -1 for other shapes
+    int chain;  // the triangle's gate-chain code (DevTri::chain)
     double u, v;
 };
 
@@ -322,6 +325,7 @@ __device__ __forceinline__ bool ray_box_ref(d4 o, d4 d, d4 r, const double* mn, 
 // the reference's dot() products multiply a cross() result whose w is exactly 0.
 __device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o, d4 d);
 
+template <bool kVerify>
 __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 o, d4 d, int slot, int key, Hit& h,
                                          int& vchain) {
     const double e1x = T.e1[0], e1y = T.e1[1], e1z = T.e1[2];
@@ -356,18 +360,19 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 
     const double t = f * dt;
     const int n = T.n;
     if (better_tri(h, t, key, n)) {
-        // Admit the hit only if the reference would have tested this triangle:
-        // its gate chain (root -> its node) passes the exact line-box tests.
         const int c = T.chain;
-        if (c != vchain) {
-#if !(defined(PTMI_EXP) && (PTMI_EXP & 8))
+        // Eager mode admits the hit only if the reference would have tested this
+        // triangle: its gate chain (root -> its node) passes the exact line-box
+        // tests.  The fast mode takes it tentatively; group_walks verifies the
+        // final winner.
+        if (kVerify && c != vchain) {
             if (!verify_chain(S, c, o, d)) {
-                PTMI_COUNT(5);  // (stats build: gate rejections; chain box count is not tallied)
+                PTMI_COUNT(5);  // (stats build: gate rejections)
                 return;
             }
-#endif
             vchain = c;
         }
+        h.chain = c;
         h.t = t;
         h.obj = slot;
         h.key = key;
@@ -411,6 +416,7 @@ __device__ __forceinline__ bool cull_box(d4 o, d4 r, double mnx, double mny, dou
 // child first, the others pushed far-to-near.  Which triangles are FOUND does
 // not depend on the visiting order or the widened boxes (every triangle that
 // can produce a winning t is reached); ties resolve through better_tri.
+template <bool kVerify>
 __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const RootRec& R, int slot,
                                            int key, d4 o, d4 d, Hit& h, int& vchain) {
     // FP32 slab tests.  With of = (float)o, rf = (float)(1/d) (|rf| clamped to
@@ -481,7 +487,7 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
             for (int i = first; i < end; i++) {
                 PTMI_COUNT(3);
 #if !(defined(PTMI_EXP) && (PTMI_EXP & 4))
-                tri_test(S, S.tris[i], o, d, slot, key, h, vchain);
+                tri_test<kVerify>(S, S.tris[i], o, d, slot, key, h, vchain);
 #endif
             }
         }
@@ -512,11 +518,11 @@ __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int ke
         // a > 0 and sq >= 0 give t1 <= t2 after rounding (rounding is monotonic),
         // so t2 can only be recorded as the winner when t1 itself is not a
         // candidate (t1 <= EPSILON); a tie t2 == t1 never replaces t1.
-        double sq = sqrt(disc);
-        double t1 = (-b - sq) / (2 * a);
+        double sq = (PTMI_ABLATE & 128) ? __builtin_amdgcn_sqrt(disc) : sqrt(disc);  // DIAGNOSTIC 128
+        double t1 = (PTMI_ABLATE & 128) ? (-b - sq) * __builtin_amdgcn_rcp(2 * a) : (-b - sq) / (2 * a);
         consider_sel(h, t1, slot, key);
         if (!(t1 > kEps)) {
-            double t2 = (-b + sq) / (2 * a);
+            double t2 = (PTMI_ABLATE & 128) ? (-b + sq) * __builtin_amdgcn_rcp(2 * a) : (-b + sq) / (2 * a);
             consider_sel(h, t2, slot, key);
         }
     }
@@ -527,13 +533,13 @@ __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int ke
 template <int FL>
 __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 rd) {
     constexpr bool A = !(FL & F_PROJ);
-    Hit h{1024.0, -1, -1, -1, 0.0, 0.0};
+    Hit h{1024.0, -1, -1, -1, -1, 0.0, 0.0};
     for (int p = 0; p < ((PTMI_ABLATE & 8) ? 0 : S.n_planes); p++) {  // intersectPlane (478-483): row 1 only
         const PlaneRec& P = S.planes[p];
         const double oy = ((P.row1[0] * ro.x + P.row1[1] * ro.y) + P.row1[2] * ro.z) + (A ? P.row1[3] : P.row1[3] * ro.w);
         const double dy0 = (P.row1[0] * rd.x + P.row1[1] * rd.y) + P.row1[2] * rd.z;
         const double dy = A ? dy0 : dy0 + P.row1[3] * rd.w;
-        const double q = -oy / dy;
+        const double q = (PTMI_ABLATE & 64) ? -oy * __builtin_amdgcn_rcp(dy) : -oy / dy;  // DIAGNOSTIC 64
         consider_sel(h, fabs(dy) > kEps ? q : 0.0, P.slot, P.key);
     }
     for (int q = 0; q < ((PTMI_ABLATE & 16) ? 0 : S.n_spheres_st); q++) {  // scale+translate spheres
@@ -622,8 +628,11 @@ __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd
     return false;
 }
 
-template <bool A>
-__device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
+// The walks of every group object for one ray.  kVerify: eager gate checks on
+// each improving candidate (exact by construction, slower: the check runs
+// inside the divergent walk loop).
+template <bool A, bool kVerify>
+__device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
 #if defined(PTMI_EXP) && (PTMI_EXP & 1)
     return;
 #endif
@@ -643,8 +652,34 @@ __device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__
             if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
                          R.hull_mx[2], h.t + prune_margin(h.t), tn))
                 continue;
-            walk_index(S, stk, R, j, ob.key, o, d, h, vchain);
+            walk_index<kVerify>(S, stk, R, j, ob.key, o, d, h, vchain);
         }
+    }
+}
+
+
+// Deferred gate verification.  The walks first take every Moller-Trumbore hit
+// tentatively; their winner is the minimum over a SUPERSET of the reference's
+// candidates, so if it passes its own gate chain it is the reference's winner.
+// Only then (a lane whose winner fails -- seen only with degenerate boxes, see
+// tests/adversarial.py) are this ray's walks redone with eager checks.  All
+// lanes verify together after the loop instead of one by one inside it.
+template <bool A>
+__device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
+    const Hit h0 = h;
+    group_walks_impl<A, false>(S, stk, ro, rd, h);
+    if (h.tri >= 0) {  // the winner is a triangle (h0 holds primitives only)
+        PTMI_COUNT(4);
+        const DevObject& ob = S.objs[h.obj];
+        const d4 o = xpt<A>(ob.inv, ob.st, ro);
+        const d4 d = xdir<A>(ob.inv, ob.st, rd);
+#if !(defined(PTMI_EXP) && (PTMI_EXP & 8))
+        if (!verify_chain(S, h.chain, o, d)) {
+            PTMI_COUNT(11);  // (stats build: eager re-walks)
+            h = h0;
+            group_walks_impl<A, true>(S, stk, ro, rd, h);
+        }
+#endif
     }
 }
 
@@ -1021,6 +1056,9 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
         // which order candidates are examined (lexicographic minimum, better()).
         bool ready = false;
         Hit h;
+#if PTMI_STATS
+        if ((FL & F_GROUPS) && (threadIdx.x & 63) == 0) atomicAdd(&ptmi_stats[10], 1ull);
+#endif
         if (active && !pending) {
             if (P.dead) {
                 h.obj = -1;
@@ -1038,6 +1076,12 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
         if (FL & F_GROUPS) {
             const int n_pend = __popcll(__ballot(pending));
             if (n_pend >= kWalkBatch || (n_pend > 0 && !__any(ready))) {
+#if PTMI_STATS
+                if ((threadIdx.x & 63) == 0) {
+                    atomicAdd(&ptmi_stats[8], 1ull);
+                    atomicAdd(&ptmi_stats[9], (unsigned long long)n_pend);
+                }
+#endif
                 if (pending) {
                     h = hp;
                     group_walks<A>(S, stk, P.ro, P.rd, h);
@@ -1200,9 +1244,9 @@ hipError_t launch_seeds(double* seeds, uint32_t n, uint64_t stream, hipStream_t 
 #if PTMI_STATS
 namespace ptmi {
 int stats_read(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi_stats), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi_stats), sizeof(unsigned long long) * 12) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[8] = {0};
+        unsigned long long z[12] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(ptmi_stats), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

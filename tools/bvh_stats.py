@@ -18,14 +18,17 @@ if scene.startswith("adv:"):
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 W, H = 1280, 960
 lib = api.load_library()
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 12)()
 lib.ptmi_stats_read(buf, 1)
 objs, tris, grps, cam = scene_inputs(scene, W, H)
 api.Trace(objs, tris, grps, 0, spp, cam, seeds=layout.seeds_go_float64(W * H, 3))
 lib.ptmi_stats_read(buf, 1)
-names = ["walks", "node4", "leaves", "tri_tests", "verifies", "gate_rejects", "obj_gate_pass", "group_obj_tests"]
+names = ["walks", "node4", "leaves", "tri_tests", "verifies", "gate_rejects", "obj_gate_pass", "group_obj_tests",
+         "walk_phases", "lanes_in_phases", "wave_iterations", "eager_rewalks"]
 v = dict(zip(names, buf))
 n = W * H * spp
 print(scene, "spp", spp)
+print("  lanes per walk phase %.1f, wave iterations per walk phase %.1f" % (
+    v["lanes_in_phases"] / max(v["walk_phases"], 1), v["wave_iterations"] / max(v["walk_phases"], 1)))
 for k in names:
     print("  %-16s %14d  per sample %8.3f  per walk %8.3f" % (k, v[k], v[k] / n, v[k] / max(v["walks"], 1)))
