@@ -40,13 +40,22 @@ enum {
     PTMI_ERR_ARG = -1,         /* bad sizes / NULL pointers / out-of-range indices   */
     PTMI_ERR_DEVICE = -2,      /* no such device, or not a gfx950 device            */
     PTMI_ERR_HIP = -3,         /* a HIP runtime call failed                          */
-    PTMI_ERR_UNSUPPORTED = -4, /* textured objects (read_imagef) -- not in this build */
+    PTMI_ERR_UNSUPPORTED = -4, /* input outside what this build implements (e.g. BVH too deep) */
     PTMI_ERR_NOMEM = -5
 };
 
-/* Texture arrays of ocl.Trace (textures / sphereTextures / cubeTextures: NRGBA8
- * image2d_array, ocltracer.go:228-254).  Reserved: must be NULL, or all counts 0;
- * scenes with textured objects are rejected with PTMI_ERR_UNSUPPORTED. */
+/* Texture arrays of ocl.Trace (textures / sphereTextures / cubeTextures,
+ * ocltracer.go:178-183, 228-254): array k holds count[k] layers of
+ * width[k] x height[k] NRGBA8 pixels (image.NRGBA.Pix, rows top to bottom), the
+ * layers concatenated in slice order -- exactly the bytes prepareTextures hands
+ * to clCreateImage.  [0] backs plane colours and plane normal maps, [1] sphere
+ * colours (sphericalMap), [2] cube colours (cubeUV cross), tracer.cl:907-914,
+ * 1077-1092.  A NULL struct or count 0 is the reference's all-zero fake image.
+ * Sampling follows the kernel's sampler (tracer.cl:829): normalized
+ * coordinates, CLK_ADDRESS_REPEAT, CLK_FILTER_LINEAR, UNORM8 -> c/255, layer =
+ * clamp(rint(index), 0, count-1) -- in software (OpenCL 1.2 s8.2 formulas, FP32):
+ * gfx950 has no image instructions (DESIGN.md "Textures").  Pixels are copied to the
+ * device during the call; the pointers are not retained. */
 typedef struct ptmi_textures {
     const uint8_t* pixels[3];
     uint32_t width[3], height[3], count[3];
@@ -107,6 +116,11 @@ typedef struct ptmi_scene ptmi_scene;
 int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, const void* triangles,
                       uint32_t n_tri, const void* groups, uint32_t n_grp, const void* camera,
                       ptmi_scene** out, char* err, size_t err_len);
+/* ptmi_scene_create with the scene's texture arrays (see ptmi_textures; NULL =
+ * no textures).  ptmi_scene_create(...) == ptmi_scene_create_textured(..., NULL, ...). */
+int ptmi_scene_create_textured(int device_index, const void* objects, uint32_t n_obj, const void* triangles,
+                               uint32_t n_tri, const void* groups, uint32_t n_grp, const void* camera,
+                               const ptmi_textures* textures, ptmi_scene** out, char* err, size_t err_len);
 void ptmi_scene_destroy(ptmi_scene* s);
 int ptmi_scene_size(const ptmi_scene* s, uint32_t* width, uint32_t* height);
 

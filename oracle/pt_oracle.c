@@ -24,8 +24,13 @@
  *   - intersections are reduced on the fly (first t > EPSILON strictly below
  *     the running best, in the reference's recording order, tracer.cl:728-739)
  *     instead of being stored in the 64-entry ctx, whose overflow is UB there.
- *   - textured objects are rejected (read_imagef, tracer.cl:907-914/1077-1092, is a
- *     later row of the scope table).
+ *   - textures (read_imagef, tracer.cl:907-914/1077-1092): the kernel's sampler
+ *     (tracer.cl:829: normalized coords, REPEAT, LINEAR, RGBA UNORM8) is restated
+ *     with the OpenCL 1.2 s8.2 formulas in FP32, separately rounded in the same
+ *     order as the HIP kernel.  PARITY UNPINNED for the sampler: gfx950 has no
+ *     image instructions, so the reference kernel cannot sample a texture on this
+ *     hardware (DESIGN.md "Textures"); sphericalMap's atan2/acos are glibc here and
+ *     ocml on the GPU (last-ulp differences, invisible after the float cast).
  */
 #include <math.h>
 #include <stdint.h>
@@ -139,8 +144,16 @@ typedef struct {
     d4 bb_min, bb_max;
     int32_t child_count;
     int32_t children[64];
-    uint8_t is_textured, is_textured_nm;
+    uint8_t is_textured, is_textured_nm, texture_index, texture_index_nm;
+    double texture_scale[4]; /* X, Y, XNM, YNM (ocltracer.go:36-39) */
 } object_t;
+
+/* One image2d_array_t of the kernel (tracer.cl:833): n layers of w x h NRGBA8
+ * texels (prepareTextures, ocltracer.go:228-254); n == 0: the all-zero fake image. */
+typedef struct {
+    const uint8_t* pix;
+    uint32_t w, h, n;
+} tex_t;
 
 typedef struct {
     d4 bb_min, bb_max;
@@ -174,7 +187,10 @@ static void unpack_object(const uint8_t* b, object_t* o) {
     memcpy(&o->child_count, b + 584, 4);
     memcpy(o->children, b + 588, 256);
     o->is_textured = b[844];
+    o->texture_index = b[845];
     o->is_textured_nm = b[846];
+    o->texture_index_nm = b[847];
+    memcpy(o->texture_scale, b + 488, 32);
 }
 
 static void unpack_group(const uint8_t* b, group_t* g) {
@@ -214,7 +230,95 @@ typedef struct {
     const tri_t* tris;
     uint32_t n_tri;
     camera_t cam;
+    tex_t tex[3]; /* textures, sphereTextures, cubeMapTextures */
 } scene_t;
+
+/* ---------------- textures (tracer.cl:113-213, 829) -------------------------- */
+typedef struct { float r, g, b; } rgb_t;
+
+/* CLK_ADDRESS_REPEAT + CLK_FILTER_LINEAR along one axis (OpenCL 1.2 s8.2). */
+static void tex_axis(float s, int n, int* i0, int* i1, float* a) {
+    if (!isfinite(s)) s = 0.0f; /* undefined in OpenCL; pinned to 0 (same as the HIP kernel) */
+    float u = (s - floorf(s)) * (float)n;
+    float um = u - 0.5f;
+    float fl = floorf(um);
+    *i0 = (int)fl;
+    *i1 = *i0 + 1;
+    if (*i0 < 0) *i0 = n + *i0;
+    if (*i1 > n - 1) *i1 = *i1 - n;
+    *a = um - fl;
+}
+
+static rgb_t texel(const tex_t* T, int l, int i, int j) {
+    const uint8_t* p = T->pix + 4 * (((size_t)l * T->h + (size_t)j) * T->w + (size_t)i);
+    rgb_t c = {(float)p[0] / 255.0f, (float)p[1] / 255.0f, (float)p[2] / 255.0f};
+    return c;
+}
+
+/* read_imagef(array, sampler, (float4)(s, t, layer, 0)).xyz */
+static rgb_t tex_sample(const tex_t* T, float s, float t, float layer) {
+    rgb_t z = {0.0f, 0.0f, 0.0f};
+    if (T->n == 0) return z;
+    int l = (int)fminf(fmaxf(rintf(layer), 0.0f), (float)(T->n - 1));
+    int i0, i1, j0, j1;
+    float a, b;
+    tex_axis(s, (int)T->w, &i0, &i1, &a);
+    tex_axis(t, (int)T->h, &j0, &j1, &b);
+    rgb_t t00 = texel(T, l, i0, j0), t10 = texel(T, l, i1, j0), t01 = texel(T, l, i0, j1), t11 = texel(T, l, i1, j1);
+    float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+    rgb_t c = {((w00 * t00.r + w10 * t10.r) + w01 * t01.r) + w11 * t11.r,
+               ((w00 * t00.g + w10 * t10.g) + w01 * t01.g) + w11 * t11.g,
+               ((w00 * t00.b + w10 * t10.b) + w01 * t01.b) + w11 * t11.b};
+    return c;
+}
+
+/* OpenCL length(double4) (opencl.bc _Z6lengthDv4_d): sqrt(dot) with range scaling. */
+static double length4(d4 v) {
+    double d = dot4(v, v);
+    if (d < 0x1p-1022) {
+        d4 p = scl4(v, 0x1p563);
+        return sqrt(dot4(p, p)) * 0x1p-563;
+    }
+    if (d == INFINITY) {
+        d4 p = scl4(v, 0x1p-514);
+        return sqrt(dot4(p, p)) * 0x1p514;
+    }
+    return sqrt(d);
+}
+
+/* sphericalMap (tracer.cl:178-213). */
+static void spherical_map(d4 p, double* u, double* v) {
+    double theta = atan2(p.x, p.z);
+    double radius = length4(mk(p.x, p.y, p.z, 0.0));
+    double phi = acos(p.y / radius);
+    double raw_u = theta / (2.0 * PI);
+    *u = 1 - (raw_u + 0.5);
+    *v = 1 - phi / PI;
+}
+
+/* cubeUV and the six cubeUV*Cross faces (tracer.cl:113-175). */
+static void cube_uv(d4 p, double* u, double* v) {
+    double coord = maxX(fabs(p.x), fabs(p.y), fabs(p.z));
+    if (coord == p.x) { /* right */
+        *u = 0.5 + fmod(1.0 - p.z, 2) / 2.0 * 0.25;
+        *v = 0.6666666 - fmod(p.y + 1.0, 2) / 2.0 * 0.333333;
+    } else if (coord == -p.x) { /* left */
+        *u = fmod(p.z + 1.0, 2) / 2.0 * 0.25;
+        *v = 0.6666666 - fmod(p.y + 1.0, 2) / 2.0 * 0.333333;
+    } else if (coord == p.y) { /* up */
+        *u = 0.25 + fmod(p.x + 1.0, 2) / 2.0 * 0.25;
+        *v = 1.0 - fmod(1.0 - p.z, 2) / 2.0 * 0.333333;
+    } else if (coord == -p.y) { /* down */
+        *u = 0.25 + fmod(p.x + 1.0, 2) / 2.0 * 0.25;
+        *v = fmod(p.z + 1.0, 2) / 2.0 * 0.333333;
+    } else if (coord == p.z) { /* front */
+        *u = 0.25 + fmod(p.x + 1.0, 2) / 2.0 * 0.25;
+        *v = 0.6666666 - fmod(p.y + 1.0, 2) / 2.0 * 0.333333;
+    } else { /* back */
+        *u = 0.75 + fmod(1.0 - p.x, 2) / 2.0 * 0.25;
+        *v = 0.6666666 - fmod(p.y + 1.0, 2) / 2.0 * 0.333333;
+    }
+}
 
 /* ---------------- intersectors --------------------------------------------- */
 
@@ -486,7 +590,12 @@ static d4 trace_pixel(const scene_t* S, const double* seeds, uint32_t i, uint32_
             d4 pos = add4(ro, scl4(rd, h.t));
             d4 eye = neg4(rd);
             d4 on;
-            if (ob->type == 0) {
+            if (ob->type == 0 && ob->is_textured_nm) { /* normal map (tracer.cl:907-911) */
+                d4 lp = mat_mul(ob->inverse, pos);
+                rgb_t c = tex_sample(&S->tex[0], (float)(fabs(lp.x) * ob->texture_scale[2]),
+                                     (float)(fabs(lp.z) * ob->texture_scale[3]), (float)ob->texture_index_nm);
+                on = normalize4(mk((double)c.r, (double)c.g, (double)c.b, 0.0));
+            } else if (ob->type == 0) {
                 on = mk(0.0, 1.0, 0.0, 0.0);
             } else if (ob->type == 1) {
                 CNT(EV_NRM_SPHERE);
@@ -577,6 +686,23 @@ static d4 trace_pixel(const scene_t* S, const double* seeds, uint32_t i, uint32_
             } else {
                 bn->color = ob->color;
                 bn->emission = ob->emission;
+                if (ob->is_textured && (ob->type == 0 || ob->type == 1 || ob->type == 3)) { /* tracer.cl:1077-1092 */
+                    d4 lp = mat_mul(ob->inverse, pos);
+                    rgb_t c;
+                    if (ob->type == 0) {
+                        c = tex_sample(&S->tex[0], (float)(lp.x * ob->texture_scale[0]),
+                                       (float)(lp.z * ob->texture_scale[1]), (float)ob->texture_index);
+                    } else if (ob->type == 1) {
+                        double u, v;
+                        spherical_map(lp, &u, &v);
+                        c = tex_sample(&S->tex[1], (float)u, (float)(1.0 - v), (float)ob->texture_index);
+                    } else {
+                        double u, v;
+                        cube_uv(lp, &u, &v);
+                        c = tex_sample(&S->tex[2], (float)u, (float)v, (float)ob->texture_index);
+                    }
+                    bn->color = mk((double)c.r, (double)c.g, (double)c.b, 1.0);
+                }
             }
             if (!entering && !exiting && !reflecting) effective++;
             actual++;
@@ -607,10 +733,12 @@ static d4 trace_pixel(const scene_t* S, const double* seeds, uint32_t i, uint32_
 /* Renders rows [row0, row0+rows) of the frame.  With the full sample range the
  * output is the reference's RGBA (colors * 1/samples, alpha 1, tracer.cl:1184-1187);
  * with a partial range it is the un-normalised RGB sum and alpha = #samples.
- * Returns 0, or <0 for unsupported input (textures: -5). */
-int pto_trace(const void* objects, uint32_t n_obj, const void* tris, uint32_t n_tri, const void* groups,
-              uint32_t n_grp, const void* camera, uint32_t samples, const double* seeds, uint32_t row0,
-              uint32_t rows, uint32_t s0, uint32_t s1, int threads, double* out) {
+ * `tex_pix/w/h/n` (may be NULL): the three texture arrays (ptmi_textures layout).
+ * Returns 0, or <0 for bad input. */
+int pto_trace_tex(const void* objects, uint32_t n_obj, const void* tris, uint32_t n_tri, const void* groups,
+                  uint32_t n_grp, const void* camera, uint32_t samples, const double* seeds, uint32_t row0,
+                  uint32_t rows, uint32_t s0, uint32_t s1, int threads, const uint8_t* const* tex_pix,
+                  const uint32_t* tex_w, const uint32_t* tex_h, const uint32_t* tex_n, double* out) {
     if (n_obj == 0 || n_obj > 16 || samples == 0 || s1 > samples || s0 > s1) return -1;
     object_t* ob = (object_t*)calloc(n_obj, sizeof(object_t));
     group_t* gr = (group_t*)calloc(n_grp ? n_grp : 1, sizeof(group_t));
@@ -619,7 +747,16 @@ int pto_trace(const void* objects, uint32_t n_obj, const void* tris, uint32_t n_
     int rc = 0;
     for (uint32_t i = 0; i < n_obj; i++) {
         unpack_object((const uint8_t*)objects + 1024u * i, &ob[i]);
-        if (ob[i].is_textured || ob[i].is_textured_nm) rc = -5;
+    }
+    for (int k = 0; k < 3; k++) {
+        S.tex[k].pix = NULL;
+        S.tex[k].w = S.tex[k].h = S.tex[k].n = 0;
+        if (tex_pix && tex_n[k] && tex_pix[k] && tex_w[k] && tex_h[k]) {
+            S.tex[k].pix = tex_pix[k];
+            S.tex[k].w = tex_w[k];
+            S.tex[k].h = tex_h[k];
+            S.tex[k].n = tex_n[k];
+        }
     }
     for (uint32_t i = 0; i < n_grp; i++) unpack_group((const uint8_t*)groups + 256u * i, &gr[i]);
     for (uint32_t i = 0; i < n_tri; i++) unpack_tri((const uint8_t*)tris + 512u * i, &tr[i]);
@@ -681,6 +818,23 @@ int pto_trace(const void* objects, uint32_t n_obj, const void* tris, uint32_t n_
     free(tr);
     return rc;
 }
+
+int pto_trace(const void* objects, uint32_t n_obj, const void* tris, uint32_t n_tri, const void* groups,
+              uint32_t n_grp, const void* camera, uint32_t samples, const double* seeds, uint32_t row0,
+              uint32_t rows, uint32_t s0, uint32_t s1, int threads, double* out) {
+    return pto_trace_tex(objects, n_obj, tris, n_tri, groups, n_grp, camera, samples, seeds, row0, rows, s0, s1,
+                         threads, NULL, NULL, NULL, NULL, out);
+}
+
+/* Texture helpers exported for the unit tests (sampler and UV maps alone). */
+void pto_tex_sample(const uint8_t* pix, uint32_t w, uint32_t h, uint32_t n, float s, float t, float layer,
+                    float* rgb) {
+    tex_t T = {pix, w, h, n};
+    rgb_t c = tex_sample(&T, s, t, layer);
+    rgb[0] = c.r, rgb[1] = c.g, rgb[2] = c.b;
+}
+void pto_spherical_map(double x, double y, double z, double* uv) { spherical_map(mk(x, y, z, 1.0), &uv[0], &uv[1]); }
+void pto_cube_uv(double x, double y, double z, double* uv) { cube_uv(mk(x, y, z, 1.0), &uv[0], &uv[1]); }
 
 float pto_noise3d(float x, float y, float z) { return noise3d(x, y, z); }
 

@@ -81,6 +81,14 @@ def _cpu_lib():
                                    ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                    ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                    ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
+        _cpu.pto_trace_tex.restype = ctypes.c_int
+        _cpu.pto_trace_tex.argtypes = _cpu.pto_trace.argtypes[:-1] + [ctypes.c_void_p] * 4 + [ctypes.c_void_p]
+        _cpu.pto_tex_sample.restype = None
+        _cpu.pto_tex_sample.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+        for f in (_cpu.pto_spherical_map, _cpu.pto_cube_uv):
+            f.restype = None
+            f.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
         _cpu.pto_noise3d.restype = ctypes.c_float
         _cpu.pto_noise3d.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float]
         _cpu.pto_sinf32.restype = ctypes.c_float
@@ -90,12 +98,48 @@ def _cpu_lib():
     return _cpu
 
 
+def _tex_arrays(tex_lists):
+    """[textures, sphereTextures, cubeTextures] (lists of H x W x 4 uint8 NRGBA
+    images) -> stacked arrays (kept alive by the caller) + ctypes arguments."""
+    keep, pix = [], (ctypes.c_void_p * 3)()
+    w, h, n = (ctypes.c_uint32 * 3)(), (ctypes.c_uint32 * 3)(), (ctypes.c_uint32 * 3)()
+    for k, imgs in enumerate(tex_lists or (None, None, None)):
+        if imgs is None or len(imgs) == 0:
+            continue
+        a = np.ascontiguousarray(np.stack([np.asarray(i, dtype=np.uint8) for i in imgs]))
+        keep.append(a)
+        pix[k] = a.ctypes.data
+        n[k], h[k], w[k] = a.shape[0], a.shape[1], a.shape[2]
+    return keep, (pix, w, h, n)
+
+
+def tex_sample(images, s, t, layer):
+    """The restated sampler alone: read_imagef(array, sampler, (s, t, layer, 0)).xyz."""
+    keep, (pix, w, h, n) = _tex_arrays([images, None, None])
+    out = (ctypes.c_float * 3)()
+    _cpu_lib().pto_tex_sample(pix[0], w[0], h[0], n[0], s, t, layer, out)
+    return tuple(out)
+
+
+def spherical_map(x, y, z):
+    uv = (ctypes.c_double * 2)()
+    _cpu_lib().pto_spherical_map(x, y, z, uv)
+    return uv[0], uv[1]
+
+
+def cube_uv(x, y, z):
+    uv = (ctypes.c_double * 2)()
+    _cpu_lib().pto_cube_uv(x, y, z, uv)
+    return uv[0], uv[1]
+
+
 def cpu_trace(objects, triangles, groups, camera, samples, seeds, row0=0, rows=None,
-              sample_begin=0, sample_end=None, threads=0):
+              sample_begin=0, sample_end=None, threads=0, textures=None):
     """C restatement of the reference kernel.  Returns float64 RGBA for rows
     [row0, row0+rows).  ``sample_begin/end`` select a sub-range of the S samples
     (global indices, as a multi-GPU sample split passes them); with a partial
-    range the result is the un-normalised sum (like one GPU's partial frame)."""
+    range the result is the un-normalised sum (like one GPU's partial frame).
+    ``textures``: [textures, sphereTextures, cubeTextures] image lists or None."""
     lib = _cpu_lib()
     cam = np.asarray(camera).reshape(())
     w, h = int(cam["width"]), int(cam["height"])
@@ -108,9 +152,10 @@ def cpu_trace(objects, triangles, groups, camera, samples, seeds, row0=0, rows=N
     triangles, pt = _as_bytes_ptr(triangles)
     groups, pg = _as_bytes_ptr(groups)
     cam_arr, pc = _as_bytes_ptr(cam)
-    rc = lib.pto_trace(po, len(objects), pt, len(triangles), pg, len(groups), pc, samples,
-                       seeds.ctypes.data_as(ctypes.c_void_p), row0, rows, sample_begin, sample_end,
-                       threads, out.ctypes.data_as(ctypes.c_void_p))
+    keep, (tp, tw, th, tn) = _tex_arrays(textures)
+    rc = lib.pto_trace_tex(po, len(objects), pt, len(triangles), pg, len(groups), pc, samples,
+                           seeds.ctypes.data_as(ctypes.c_void_p), row0, rows, sample_begin, sample_end,
+                           threads, tp, tw, th, tn, out.ctypes.data_as(ctypes.c_void_p))
     if rc != 0:
         raise RuntimeError("pto_trace rc=%d" % rc)
     return out

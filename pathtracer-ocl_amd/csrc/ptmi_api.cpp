@@ -37,7 +37,7 @@ using namespace ptmi;
 struct ptmi_scene {
     int device = 0;
     DevScene dev{};
-    void* buffers[10] = {};
+    void* buffers[13] = {};  // [10..12]: texture arrays
     double* partial = nullptr;  // chunk partial sums, grown on demand
     double* sunf = nullptr;     // DoF aperture table for sunf_samples (sunflower_kernel)
     uint32_t sunf_samples = 0;
@@ -159,13 +159,11 @@ int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, u
         o.st = is_st_pattern(o.inv) ? 1 : 0;
         o.invt_diag = is_diag3(o.inv_t) ? 1 : 0;
         std::memcpy(o.bb_max, b + 552, 32);
-        if (b[844] || b[846]) {
-            set_err(err, err_len,
-                    "object %u is textured (isTextured/isTexturedNM): read_imagef textures are not supported "
-                    "by this build",
-                    i);
-            return PTMI_ERR_UNSUPPORTED;
-        }
+        o.tex = b[844] ? 1 : 0;  // isTextured, textureIndex, isTexturedNM, textureIndexNM (ocltracer.go:44-47)
+        o.tex_index = b[845];
+        o.tex_nm = b[846] ? 1 : 0;
+        o.tex_index_nm = b[847];
+        std::memcpy(o.tex_scale, b + 488, 32);  // textureScaleX, Y, XNM, YNM (ocltracer.go:36-39)
         o.child_count = 0;
         o.child_base = (int32_t)roots.size();
         if (o.type == 4) {
@@ -276,6 +274,13 @@ const char* ptmi_build_info(void) {
 int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
                       const void* groups, uint32_t n_grp, const void* camera, ptmi_scene** out, char* err,
                       size_t err_len) {
+    return ptmi_scene_create_textured(device_index, objects, n_obj, triangles, n_tri, groups, n_grp, camera, nullptr,
+                                      out, err, err_len);
+}
+
+int ptmi_scene_create_textured(int device_index, const void* objects, uint32_t n_obj, const void* triangles,
+                               uint32_t n_tri, const void* groups, uint32_t n_grp, const void* camera,
+                               const ptmi_textures* textures, ptmi_scene** out, char* err, size_t err_len) {
     if (!out) {
         set_err(err, err_len, "out == NULL");
         return PTMI_ERR_ARG;
@@ -312,7 +317,24 @@ int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, con
     for (const DevTriShade& t : st)
         affine = affine && std::isfinite(t.n1[3]) && std::isfinite(t.n2[3]) && std::isfinite(t.n3[3]);
     if (!affine) flags |= 16;                                           // F_PROJ
-    if (const char* f = getenv("PTMI_FORCE_FLAGS")) flags = atoi(f) & 31;  // testing: force the generic path
+    // Textured plane/sphere/cube colours or plane normal maps: the one textured
+    // instantiation (generic arithmetic + software sampler, tracer.cl:907-914, 1077-1092).
+    for (const DevObject& o : objs)
+        if ((o.tex && (o.type == 0 || o.type == 1 || o.type == 3)) || (o.tex_nm && o.type == 0)) flags = 63;
+    if (const char* f = getenv("PTMI_FORCE_FLAGS")) flags = atoi(f) & 63;  // testing: force the generic path
+    if (textures) {
+        for (int k = 0; k < 3; k++) {
+            const uint64_t texels = (uint64_t)textures->width[k] * textures->height[k] * textures->count[k];
+            if (textures->count[k] &&
+                (!textures->pixels[k] || textures->width[k] == 0 || textures->height[k] == 0 ||
+                 textures->width[k] > (1u << 16) || textures->height[k] > (1u << 16) || textures->count[k] > 256 ||
+                 texels > ((uint64_t)1 << 32))) {
+                set_err(err, err_len, "texture array %d: bad size %ux%u x %u layers (or NULL pixels)", k,
+                        textures->width[k], textures->height[k], textures->count[k]);
+                return PTMI_ERR_ARG;
+            }
+        }
+    }
     HIP_TRY(hipSetDevice(device_index));
     ptmi_scene* s = new ptmi_scene();
     s->flags = flags;
@@ -326,6 +348,23 @@ int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, con
         (rc = upload(root_rec, &s->buffers[9], err, err_len))) {
         ptmi_scene_destroy(s);
         return rc;
+    }
+    for (int k = 0; k < 3; k++) {  // texture arrays (prepareTextures, ocltracer.go:228-254)
+        DevTexArray& T = s->dev.tex[k];
+        T = DevTexArray{};
+        if (!textures || textures->count[k] == 0) continue;  // the all-zero fake image
+        const size_t bytes = (size_t)textures->width[k] * textures->height[k] * textures->count[k] * 4;
+        hipError_t e = hipMalloc(&s->buffers[10 + k], bytes);
+        if (e == hipSuccess) e = hipMemcpy(s->buffers[10 + k], textures->pixels[k], bytes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            set_err(err, err_len, "texture array %d upload (%zu B): %s", k, bytes, hipGetErrorString(e));
+            ptmi_scene_destroy(s);
+            return PTMI_ERR_HIP;
+        }
+        T.texels = (const uint32_t*)s->buffers[10 + k];
+        T.w = (int32_t)textures->width[k];
+        T.h = (int32_t)textures->height[k];
+        T.layers = (int32_t)textures->count[k];
     }
     s->dev.objs = (const DevObject*)s->buffers[0];
     for (int t = 0; t < 5; t++) s->dev.run_end[t] = run_end[t];
@@ -541,20 +580,13 @@ int ptmi_fill_seeds(double* seeds_dev, uint32_t n, uint64_t seed_stream, void* h
 int ptmi_trace(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri, const void* groups,
                uint32_t n_grp, int device_index, uint32_t samples, const void* camera, const double* seeds,
                uint64_t seed_stream, const ptmi_textures* textures, double* out_rgba, char* err, size_t err_len) {
-    if (textures) {
-        for (int k = 0; k < 3; k++)
-            if (textures->count[k]) {
-                set_err(err, err_len, "texture arrays are not supported by this build");
-                return PTMI_ERR_UNSUPPORTED;
-            }
-    }
     if (!out_rgba || samples == 0) {
         set_err(err, err_len, "out_rgba == NULL or samples == 0");
         return PTMI_ERR_ARG;
     }
     ptmi_scene* s = nullptr;
-    int rc = ptmi_scene_create(device_index, objects, n_obj, triangles, n_tri, groups, n_grp, camera, &s, err,
-                               err_len);
+    int rc = ptmi_scene_create_textured(device_index, objects, n_obj, triangles, n_tri, groups, n_grp, camera,
+                                        textures, &s, err, err_len);
     if (rc) return rc;
     const uint32_t npix = s->width * s->height;
     double *d_seeds = nullptr, *d_sums = nullptr;
@@ -598,13 +630,6 @@ extern "C" int ptmi_trace_multi(const void* objects, uint32_t n_obj, const void*
                      uint32_t n_grp, const int* devices, uint32_t n_devices, int split, uint32_t samples,
                      const void* camera, const double* seeds, uint64_t seed_stream, const ptmi_textures* textures,
                      double* out_rgba, char* err, size_t err_len) {
-    if (textures) {
-        for (int k = 0; k < 3; k++)
-            if (textures->count[k]) {
-                set_err(err, err_len, "texture arrays are not supported by this build");
-                return PTMI_ERR_UNSUPPORTED;
-            }
-    }
     if (!out_rgba || samples == 0 || !devices || n_devices == 0 || (split != 0 && split != 1) || !camera) {
         set_err(err, err_len, "ptmi_trace_multi: bad arguments");
         return PTMI_ERR_ARG;
@@ -621,7 +646,8 @@ extern "C" int ptmi_trace_multi(const void* objects, uint32_t n_obj, const void*
         ptmi_scene* s = nullptr;
         double *d_seeds = nullptr, *d_sums = nullptr;
         hipStream_t st = nullptr;
-        rc = ptmi_scene_create(devices[d], objects, n_obj, triangles, n_tri, groups, n_grp, camera, &s, e, sizeof(e));
+        rc = ptmi_scene_create_textured(devices[d], objects, n_obj, triangles, n_tri, groups, n_grp, camera, textures,
+                                        &s, e, sizeof(e));
         if (!rc && (s->width != W || s->height != H)) rc = PTMI_ERR_ARG;
         if (!rc && (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
                     hipMalloc((void**)&d_seeds, npix * sizeof(double)) != hipSuccess ||

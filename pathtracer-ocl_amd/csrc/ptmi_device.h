@@ -35,7 +35,19 @@ struct alignas(16) DevObject {
     int32_t key;                  // index in the reference's object list (tie-break order)
     int32_t st;                   // inv has the scale+translate zero pattern (see xform_st)
     int32_t invt_diag;            // rows 0-2 of inv_t are diagonal
-    int32_t pad[2];
+    uint8_t tex, tex_index;       // isTextured, textureIndex (ocltracer.go:44-45)
+    uint8_t tex_nm, tex_index_nm; // isTexturedNM, textureIndexNM (planes only, tracer.cl:907-914)
+    int32_t pad;
+    double tex_scale[4];          // textureScaleX, Y, XNM, YNM (ocltracer.go:36-39)
+};
+static_assert(sizeof(DevObject) == 512, "DevObject must stay 512 B");
+
+// One texture array (image2d_array_t of tracer.cl:833): `layers` NRGBA8 images
+// of w x h texels, row-major, layers concatenated.  layers == 0: the reference's
+// all-zero fake image (ocltracer.go:249-251).
+struct DevTexArray {
+    const uint32_t* texels;
+    int32_t w, h, layers, pad;
 };
 
 // Reference BVH node (CLGroup, tracer.cl:24-35): its box gates the triangles
@@ -132,6 +144,7 @@ struct DevScene {
     uint32_t n_nodes, n_tri;
     uint32_t n_list;  // numObjects of the reference's list (fgi = seed / numObjects, tracer.cl:840)
     DevCamera cam;
+    DevTexArray tex[3];  // textures, sphereTextures, cubeMapTextures (tracer.cl:833)
 };
 
 constexpr int kTile = 8;          // a wave64 covers an 8x8 pixel tile

@@ -261,7 +261,8 @@ enum : int {
     F_MATERIALS = 4,  // reflectivity != 0 or refractive index != 1 somewhere
     F_DOF = 8,        // camera aperture != 0
     F_ALL = 15,
-    F_PROJ = 16       // not affine (see dotv): the literal double4 arithmetic, generic path only
+    F_PROJ = 16,      // not affine (see dotv): the literal double4 arithmetic, generic path only
+    F_TEX = 32        // textured objects: with F_ALL | F_PROJ, the one textured instantiation
 };
 
 // intersectRayWithBox (tracer.cl:270-280) returning the line's slab interval.
@@ -827,6 +828,128 @@ __device__ __forceinline__ void start_path(PathState& P, d4 ro, d4 rd) {
                isfinite(rd.y) && isfinite(rd.z) && (A || isfinite(rd.w)));
 }
 
+// ---- Textures (tracer.cl:113-213, 829, 907-914, 1077-1092) ----------------------
+// gfx950 has no image instructions (read_imagef does not lower for it; DESIGN.md
+// "Textures"), so the kernel's sampler -- CLK_NORMALIZED_COORDS_TRUE |
+// CLK_ADDRESS_REPEAT | CLK_FILTER_LINEAR on RGBA UNORM8 arrays -- is done here in
+// software with the OpenCL 1.2 s8.2 formulas in FP32, separately rounded in a fixed
+// order (the CPU oracle restates the same sequence; parity unpinned).
+struct Rgb {
+    float r, g, b;
+};
+
+// Repeat addressing + linear filter along one axis: texel pair and weight.
+__device__ __forceinline__ void tex_axis(float s, int n, int& i0, int& i1, float& a) {
+    if (!isfinite(s)) s = 0.0f;  // undefined in OpenCL; pinned to 0 here and in the oracle
+    const float u = (s - floorf(s)) * (float)n;
+    const float um = u - 0.5f;
+    const float fl = floorf(um);
+    i0 = (int)fl;
+    i1 = i0 + 1;
+    if (i0 < 0) i0 = n + i0;
+    if (i1 > n - 1) i1 = i1 - n;
+    a = um - fl;
+}
+
+__device__ __forceinline__ Rgb texel(const DevTexArray& T, int layer, int i, int j) {
+    const uint32_t p = T.texels[((size_t)layer * (size_t)T.h + (size_t)j) * (size_t)T.w + (size_t)i];
+    return Rgb{(float)(p & 0xffu) / 255.0f, (float)((p >> 8) & 0xffu) / 255.0f, (float)((p >> 16) & 0xffu) / 255.0f};
+}
+
+// read_imagef(array, sampler, (float4)(s, t, layer, 0)).xyz
+__device__ __noinline__ Rgb tex_sample(const DevTexArray T, float s, float t, float layer) {
+    if (T.layers <= 0) return Rgb{0.0f, 0.0f, 0.0f};  // the reference's all-zero fake image
+    const int l = (int)fminf(fmaxf(rintf(layer), 0.0f), (float)(T.layers - 1));
+    int i0, i1, j0, j1;
+    float a, b;
+    tex_axis(s, T.w, i0, i1, a);
+    tex_axis(t, T.h, j0, j1, b);
+    const Rgb t00 = texel(T, l, i0, j0), t10 = texel(T, l, i1, j0);
+    const Rgb t01 = texel(T, l, i0, j1), t11 = texel(T, l, i1, j1);
+    const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+    return Rgb{((w00 * t00.r + w10 * t10.r) + w01 * t01.r) + w11 * t11.r,
+               ((w00 * t00.g + w10 * t10.g) + w01 * t01.g) + w11 * t11.g,
+               ((w00 * t00.b + w10 * t10.b) + w01 * t01.b) + w11 * t11.b};
+}
+
+// OpenCL length(double4) (opencl.bc): sqrt(dot) with range scaling.
+__device__ __forceinline__ double length4(d4 v) {
+    const double d = dot4(v, v);
+    if (d < 0x1p-1022) return sqrt(dot4(scl4(v, 0x1p563), scl4(v, 0x1p563))) * 0x1p-563;
+    if (d == __builtin_inf()) return sqrt(dot4(scl4(v, 0x1p-514), scl4(v, 0x1p-514))) * 0x1p514;
+    return sqrt(d);
+}
+
+// sphericalMap (tracer.cl:178-213) -> (u, v)
+__device__ __noinline__ void spherical_map(d4 p, double& u, double& v) {
+    const double theta = atan2(p.x, p.z);
+    const double radius = length4(mk(p.x, p.y, p.z, 0.0));
+    const double phi = acos(p.y / radius);
+    const double raw_u = theta / (2.0 * kPi);
+    u = 1 - (raw_u + 0.5);
+    v = 1 - phi / kPi;
+}
+
+// cubeUV (tracer.cl:113-175): the face of a 4x3 cross layout -> (u, v)
+__device__ __noinline__ void cube_uv(d4 p, double& u, double& v) {
+    const double coord = max3(fabs(p.x), fabs(p.y), fabs(p.z));
+    double fu, fv;
+    if (coord == p.x) {  // right
+        fu = fmod(1.0 - p.z, 2.0) / 2.0, fv = fmod(p.y + 1.0, 2.0) / 2.0;
+        u = 0.5 + fu * 0.25, v = 0.6666666 - fv * 0.333333;
+    } else if (coord == -p.x) {  // left
+        fu = fmod(p.z + 1.0, 2.0) / 2.0, fv = fmod(p.y + 1.0, 2.0) / 2.0;
+        u = fu * 0.25, v = 0.6666666 - fv * 0.333333;
+    } else if (coord == p.y) {  // up
+        fu = fmod(p.x + 1.0, 2.0) / 2.0, fv = fmod(1.0 - p.z, 2.0) / 2.0;
+        u = 0.25 + fu * 0.25, v = 1.0 - fv * 0.333333;
+    } else if (coord == -p.y) {  // down
+        fu = fmod(p.x + 1.0, 2.0) / 2.0, fv = fmod(p.z + 1.0, 2.0) / 2.0;
+        u = 0.25 + fu * 0.25, v = fv * 0.333333;
+    } else if (coord == p.z) {  // front
+        fu = fmod(p.x + 1.0, 2.0) / 2.0, fv = fmod(p.y + 1.0, 2.0) / 2.0;
+        u = 0.25 + fu * 0.25, v = 0.6666666 - fv * 0.333333;
+    } else {  // back
+        fu = fmod(1.0 - p.x, 2.0) / 2.0, fv = fmod(p.y + 1.0, 2.0) / 2.0;
+        u = 0.75 + fu * 0.25, v = 0.6666666 - fv * 0.333333;
+    }
+}
+
+// Texture colour of a textured plane / sphere / cube hit (tracer.cl:1077-1092)
+// from T = the array of its type; false for other types (the object colour stays).
+template <bool A>
+__device__ __noinline__ bool textured_color(const DevTexArray T, const DevObject& ob, d4 pos, double& r, double& g,
+                                            double& b) {
+    const d4 lp = xpt<A>(ob.inv, ob.st, pos);
+    Rgb c;
+    if (ob.type == 0) {
+        c = tex_sample(T, (float)(lp.x * ob.tex_scale[0]), (float)(lp.z * ob.tex_scale[1]),
+                       (float)ob.tex_index);
+    } else if (ob.type == 1) {
+        double u, v;
+        spherical_map(lp, u, v);
+        c = tex_sample(T, (float)u, (float)(1.0 - v), (float)ob.tex_index);
+    } else if (ob.type == 3) {
+        double u, v;
+        cube_uv(lp, u, v);
+        c = tex_sample(T, (float)u, (float)v, (float)ob.tex_index);
+    } else {
+        return false;
+    }
+    r = (double)c.r, g = (double)c.g, b = (double)c.b;
+    return true;
+}
+
+// Normal-mapped plane: objectNormal = normalize(rgb of the normal map, 0)
+// (tracer.cl:907-911).
+template <bool A>
+__device__ __noinline__ d4 plane_normal_map(const DevTexArray T, const DevObject& ob, d4 pos) {
+    const d4 lp = xpt<A>(ob.inv, ob.st, pos);
+    const Rgb c = tex_sample(T, (float)(fabs(lp.x) * ob.tex_scale[2]), (float)(fabs(lp.z) * ob.tex_scale[3]),
+                             (float)ob.tex_index_nm);
+    return normalize4(mk((double)c.r, (double)c.g, (double)c.b, 0.0));
+}
+
 // One bounce (tracer.cl:884-1110).  Returns true when the path has ended.
 // One bounce of the path given its closest hit h (tracer.cl:886-1110 after
 // findClosestIntersection).  Returns true when the path has ended.
@@ -841,11 +964,13 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
     d4 eye = mk(-P.rd.x, -P.rd.y, -P.rd.z, -P.rd.w);
     // Object normal -> world normal (tracer.cl:903-955).
     d4 nv;
-    if (type == 0) {
+    if (type == 0 && !((FL & F_TEX) && ob.tex_nm)) {
         nv = ld4(ob.plane_n);  // constant per plane: normalize(mul(invT, (0,1,0,0))), w = 0
     } else {
         d4 on;
-        if (type == 1) {
+        if ((FL & F_TEX) && type == 0) {
+            on = plane_normal_map<A>(S.tex[0], ob, pos);
+        } else if (type == 1) {
             d4 lp = xpt<A>(ob.inv, ob.st, pos);
             on = mk(lp.x - 0.0, lp.y - 0.0, lp.z - 0.0, A ? 0.0 : lp.w - 1.0);
         } else if ((FL & F_CYLCUBE) && type == 2) {
@@ -931,6 +1056,9 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
             cr = ob.color[0];
             cg = ob.color[1];
             cb = ob.color[2];
+            if constexpr ((FL & F_TEX) != 0) {
+                if (ob.tex) textured_color<A>(S.tex[type == 0 ? 0 : type == 1 ? 1 : 2], ob, pos, cr, cg, cb);
+            }
         }
         P.ar = P.ar + P.mr * er;
         P.ag = P.ag + P.mg * eg;
@@ -1190,6 +1318,7 @@ __global__ __launch_bounds__(256) void seeds_kernel(double* __restrict__ seeds, 
 
 // ---- host-side launch wrappers (called from ptmi_api.cpp) ----------------------
 const void* trace_kernel_symbol(int flags) {
+    if (flags & F_TEX) return reinterpret_cast<const void*>(&trace_kernel<F_ALL | F_PROJ | F_TEX>);
     if (flags & F_PROJ) return reinterpret_cast<const void*>(&trace_kernel<F_ALL | F_PROJ>);
     switch (flags & F_ALL) {
 #define K(f) \
@@ -1205,6 +1334,11 @@ hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, uint32_t
                         const double* seeds, const double* sunf, double* out, hipStream_t st) {
     const int tiles = ((S.cam.width + kTile - 1) / kTile) * ((S.cam.height + kTile - 1) / kTile);
     dim3 grid((tiles + kWavesPerBlock - 1) / kWavesPerBlock, nchunks);
+    if (flags & F_TEX) {  // textured scene: the generic instantiation plus the texture lookups
+        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ | F_TEX>, grid, dim3(256), 0, st, S, samples, s_begin, s_end,
+                           chunk_len, tile_stride, tile_offset, seeds, sunf, out);
+        return hipGetLastError();
+    }
     if (flags & F_PROJ) {  // non-affine scene: one generic instantiation with the literal w arithmetic
         hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ>, grid, dim3(256), 0, st, S, samples, s_begin, s_end,
                            chunk_len, tile_stride, tile_offset, seeds, sunf, out);

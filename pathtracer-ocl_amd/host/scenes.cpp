@@ -23,6 +23,7 @@ constexpr double PI_OVER_2 = 1.5707963267948966;
 constexpr double PI_OVER_3 = 1.0471975511965979;
 constexpr double PI_OVER_4 = 0.7853981633974483;
 constexpr double PI_OVER_12 = 0.26179938779914946;
+constexpr double PI = 3.141592653589793;  // math.Pi
 
 struct Camera {  // camera.Camera (camera.go:8-19)
     int width = 0, height = 0;
@@ -338,6 +339,236 @@ Scene transparent_teapot_scene(Ctx& C, int w, int h, double ap, double fl) {  //
     return S;
 }
 
+Material textured(Material m, uint8_t tid, double sx = 0.0, double sy = 0.0) {  // Material.Textured ...
+    m.textured = true;
+    m.texture_id = tid;
+    m.texture_scale_x = sx;
+    m.texture_scale_y = sy;
+    return m;
+}
+Material with_nm(Material m, uint8_t tid, double sx, double sy) {  // Material.TexturedNM ...
+    m.textured_nm = true;
+    m.texture_id_nm = tid;
+    m.texture_scale_x_nm = sx;
+    m.texture_scale_y_nm = sy;
+    return m;
+}
+
+Scene textured_planets_scene(Ctx& C, int w, int h, double ap, double fl) {  // texturedplanets.go:13-135
+    Scene S{C.std_camera(w, h, ap, fl), {}};
+    Shape* left = C.A.plane();
+    left->set_transform(translate(-.6, 0, 0));
+    left->set_transform(rotate_x(PI));
+    left->set_transform(rotate_z(PI_OVER_2));
+    left->set_transform(rotate_y(PI_OVER_2));
+    left->set_material(with_nm(textured(new_diffuse(0.75, 0.25, 0.25), 0, 1.0, 1.0), 3, 1.0, 1.0));
+    Shape* right = C.A.plane();
+    right->set_transform(translate(.6, 0, 0));
+    right->set_transform(rotate_z(PI_OVER_2));
+    right->set_transform(rotate_y(PI_OVER_2));
+    right->set_material(with_nm(textured(new_diffuse(0.25, 0.25, 0.75), 0, 1.0, 1.0), 3, 1.0, 1.0));
+    Shape* floor = C.A.plane();
+    floor->set_transform(translate(0, -.4, 0));
+    floor->set_material(textured(new_diffuse(0.9, 0.8, 0.7), 1, 0.25, 0.25));
+    Shape* ceil = C.A.plane();
+    ceil->set_transform(translate(0, .4, 0));
+    ceil->set_material(textured(new_diffuse(0.9, 0.8, 0.7), 2, 1.0, 1.0));
+    Shape* back = C.A.plane();
+    back->set_transform(translate(0, 0, .4));
+    back->set_transform(rotate_x(PI_OVER_2));
+    back->set_material(with_nm(textured(new_diffuse(0.9, 0.8, 0.7), 0, 1.0, 1.0), 3, 1.0, 1.0));
+    Shape* lsp = C.sphere(-0.3, -0.1, -0.25, 0.2, textured(new_diffuse(0.9, 0.8, 0.7), 1));
+    Shape* rsp = C.A.sphere();
+    rsp->set_transform(translate(0.2, 0, -0.3));
+    rsp->set_transform(rotate_y(PI));
+    rsp->set_transform(scale(0.25, 0.25, 0.25));
+    rsp->set_material(textured(new_diffuse(0.9, 0.8, 0.7), 0));
+    Material light = new_light_bulb();
+    light.emission = color(10, 10, 10);
+    Shape* l1 = C.A.sphere();
+    l1->set_transform(translate(0, .395, -.9));
+    l1->set_transform(scale(0.283, 0.01, 0.283));
+    l1->set_material(light);
+    Shape* l2 = C.A.sphere();
+    l2->set_transform(translate(0, 0, -1.7));
+    l2->set_transform(scale(0.283, 0.283, 0.01));
+    l2->set_material(light);
+    S.objects = {l1, l2, floor, ceil, left, right, back, lsp, rsp};
+    return S;
+}
+
+Material sky_material(bool env_map) {  // envmap.go:55-61, cubemap.go:60-66
+    Material m = textured(new_default_material(), 0, 1.0, 1.0);
+    m.emission = color(1, 1, 1);
+    m.is_env_map = env_map;
+    return m;
+}
+
+Scene envmap_scene(Ctx& C, int w, int h, double ap, double fl) {  // EnvironmentMap (envmap.go:13-72)
+    Camera cam = new_camera(w, h, PI_OVER_3, point(0, 0.1, -1.5), point(0, 0.15, 0));
+    cam.focal_length = fl, cam.aperture = ap;
+    Scene S{cam, {}};
+    Shape* rsp = C.sphere(0, -0.14, -0.30, 0.16, new_mirror());
+    Shape* sky = C.A.sphere();
+    sky->set_transform(scale(5, 5, 5));
+    sky->set_material(sky_material(false));
+    S.objects = {rsp, sky};
+    return S;
+}
+
+Scene cubemap_scene(Ctx& C, int w, int h, double ap, double fl) {  // EnvironmentCubeMap (cubemap.go:15-94)
+    C.A.subgroup_counter = 0;
+    Camera cam = new_camera(w, h, PI_OVER_3, point(0, 0.3, -2.7), point(0, 0.45, 0));
+    cam.focal_length = fl, cam.aperture = ap;
+    Scene S{cam, {}};
+    Shape* rsp = C.sphere(.2, 1, 2, 0.26, new_mirror());
+    Material light = new_light_bulb();
+    light.emission = color(19.5, 19.5, 19.5);
+    Shape* lsrc = C.sphere(1.1, 1, -4, 0.7, light);
+    Shape* sky = C.A.cube();
+    sky->set_transform(translate(0, 0, 0));
+    sky->set_transform(scale(5, 5, 5));
+    sky->set_material(sky_material(true));
+    Shape* group = mesh_group(C, "gopher.obj", false);
+    group->bounds();
+    group->set_transform(translate(-.7, -0.15, 0.2));
+    group->set_transform(rotate_z(-PI_OVER_2));
+    group->set_transform(rotate_x(-PI_OVER_4));
+    group->set_transform(scale(0.4, 0.4, 0.4));
+    Material silver = new_diffuse(0.75, 0.75, 0.75);
+    silver.reflectivity = 0.0;
+    group->set_material(silver);
+    divide(C.A, group, 60);
+    group->bounds();
+    S.objects = {lsrc, rsp, sky, group};
+    return S;
+}
+
+Shape* cube_at(Ctx& C, double tx, double ty, double tz, std::initializer_list<Mat> rots, double sx, double sy,
+               double sz, const Material& m) {
+    Shape* c = C.A.cube();
+    c->set_transform(translate(tx, ty, tz));
+    for (const Mat& r : rots) c->set_transform(r);
+    c->set_transform(scale(sx, sy, sz));
+    c->set_material(m);
+    return c;
+}
+
+Scene gopher_window_scene(Ctx& C, int w, int h, double ap, double fl) {  // gopher-with-window.go:15-140
+    C.A.subgroup_counter = 0;
+    Scene S{C.std_camera(w, h, ap, fl), {}};
+    auto W = C.walls(1.4);
+    Material window = new_diffuse(0.75, 0.75, 1);
+    window.emission = color(24, 24, 24);
+    const Mat ry = rotate_y(PI_OVER_2), rx = rotate_x(PI_OVER_2);
+    const Material border = new_diffuse(0.95, 0.95, 1);
+    Shape* cube = cube_at(C, 0.6, .1, 0, {ry}, 0.1, 0.16, 0.002, window);
+    Shape* rb = cube_at(C, 0.6, .1, -0.1, {ry}, 0.01, 0.16, 0.02, border);
+    Shape* lb = cube_at(C, 0.6, .1, 0.1, {ry}, 0.01, 0.16, 0.02, border);
+    Shape* bb = cube_at(C, 0.6, -.06, 0.0, {rx, ry}, 0.01, 0.11, 0.04, border);
+    Shape* tb = cube_at(C, 0.6, .26, 0.0, {rx, ry}, 0.01, 0.11, 0.03, border);
+    Shape* csp = C.sphere(0, -0.28, -0.3, 0.12, new_diffuse(0.9, 0.8, 0.7));
+    Material half_mirror = new_mirror();
+    half_mirror.reflectivity = 0.8;
+    half_mirror.color = color(0.97, 0.97, 0.843);
+    Shape* rsp = C.sphere(0.28, -0.24, 0.15, 0.16, half_mirror);
+    S.objects = {W[2], W[3], W[0], W[1], W[4], cube, lb, rb, bb, tb, W[5], csp, rsp};
+    Shape* group = mesh_group(C, "gopher.obj", false);
+    group->bounds();
+    group->set_transform(translate(-.4, -0.15, 0.2));
+    group->set_transform(rotate_z(-PI_OVER_2));
+    group->set_transform(rotate_x(-PI_OVER_4));
+    group->set_transform(scale(0.2, 0.2, 0.2));
+    Material silver = new_diffuse(0.75, 0.75, 0.75);
+    silver.reflectivity = 0.2;
+    group->set_material(silver);
+    divide(C.A, group, 60);
+    group->bounds();
+    S.objects.push_back(group);
+    Shape* lsrc = C.A.sphere();
+    lsrc->set_transform(translate(0, 1.36, 0));
+    Material light = new_light_bulb();
+    light.emission = color(9, 8, 6);
+    lsrc->set_material(light);
+    S.objects.push_back(lsrc);
+    return S;
+}
+
+Scene christian_scene(Ctx& C, int w, int h, double ap, double fl) {  // christian.go:14-190
+    C.A.subgroup_counter = 0;
+    Scene S{C.std_camera(w, h, ap, fl), {}};
+    auto W = C.walls();
+    Shape* lsp = C.sphere(-0.35, -0.28, -0.15, 0.12, new_diffuse(0.9, 0.9, 0.9));
+    lsp->material.reflectivity = 0.99;
+    Shape* group = mesh_group(C, "teapot.obj", true);
+    group->bounds();
+    group->set_transform(translate(0, -0.4, 0));
+    group->set_transform(scale(0.07, 0.07, 0.07));
+    Material silver = new_diffuse(0.75, 0.75, 0.75);
+    silver.reflectivity = 0.2;
+    group->set_material(silver);
+    divide(C.A, group, 50);
+    group->bounds();
+    Material light = new_light_bulb();
+    light.emission = color(90, 80, 60);
+    Material cover_m = new_diffuse(0.8, 0.8, 0.8);
+    cover_m.reflectivity = 0.95;
+    auto lamp = [&](double x) { return C.sphere(x, .3, 0, 0.03, light); };
+    auto cover = [&](double x) {
+        Shape* c = C.A.cylinder(0, 1, false);
+        c->set_transform(translate(x, .295, 0));
+        c->set_transform(scale(0.06, 0.4, 0.06));
+        c->set_material(cover_m);
+        return c;
+    };
+    Shape* l2 = lamp(-0.3);
+    Shape* l3 = lamp(-0.1);
+    Shape* l4 = lamp(0.1);
+    Shape* l5 = lamp(0.3);
+    Shape* c2 = cover(-0.3);
+    Shape* c3 = cover(-0.1);
+    Shape* c4 = cover(0.1);
+    Shape* c5 = cover(0.3);
+    S.objects = {l2, l3, l4, l5, c2, c3, c4, c5, W[2], W[3], W[0], W[1], W[4], group, lsp};
+    return S;
+}
+
+// GlassScene (transparent_glass.go:15-146).  Its mesh, assets/glass.obj, is not
+// shipped with the reference: without it the build fails as Go's os.ReadFile panic.
+Scene glass_scene(Ctx& C, int w, int h, double ap, double fl) {
+    C.A.subgroup_counter = 0;
+    Scene S{C.std_camera(w, h, ap, fl), {}};
+    auto W = C.walls(.6);
+    C.label_walls(W);
+    Shape* lsp = C.sphere(-0.2, -0.28, 0.25, 0.12, new_mirror());
+    Shape* rsp = C.sphere(0.25, -0.28, 0.25, 0.12, new_glass());
+    lsp->label = "left_spr", rsp->label = "right_spr";
+    Material mtrl = new_glass();
+    mtrl.reflectivity = 0.0;
+    ObjModel model = C.load_obj("glass.obj");
+    Shape* group = model.to_group(C.A);
+    std::vector<Shape*> tris = group->children.at(0)->children;  // glass(): children 0 and 1 (:128-134)
+    const auto& t1 = group->children.at(1)->children;
+    tris.insert(tris.end(), t1.begin(), t1.end());
+    compute_vertex_normals(tris);
+    group->bounds();
+    group->set_transform(translate(-0.3, -0.395, -0.2));
+    group->set_transform(scale(0.03, 0.03, 0.03));
+    group->set_material(mtrl);
+    divide(C.A, group, 50);
+    group->bounds();
+    group->label = "glass   ";
+    S.objects = {W[2], W[3], W[0], W[1], W[4], W[5], lsp, rsp, group};
+    for (int i = 0; i < 2; i++)
+        for (int j = 0; j < 2; j++) {
+            Shape* l = C.cube_light(-0.25 + (double)i * 0.5, .4, -0.25 + (double)j * 0.5, 0.15, 0.001, 0.15,
+                                    color(10, 10, 10));
+            l->label = "light " + std::to_string(i) + "-" + std::to_string(j);
+            S.objects.push_back(l);
+        }
+    return S;
+}
+
 using Factory = std::function<Scene(Ctx&, int, int, double, double)>;
 const std::vector<std::pair<const char*, Factory>>& factories() {
     static const std::vector<std::pair<const char*, Factory>> f = {
@@ -350,6 +581,12 @@ const std::vector<std::pair<const char*, Factory>>& factories() {
         {"transparency_f_light", transparency_f_light_scene},
         {"transparent_teapot", transparent_teapot_scene},
         {"default", ocl_scene},
+        {"textures", textured_planets_scene},
+        {"envmap", envmap_scene},
+        {"cubemap", cubemap_scene},
+        {"gopher-window", gopher_window_scene},
+        {"christian", christian_scene},
+        {"glass", glass_scene},
     };
     return f;
 }
@@ -422,6 +659,20 @@ Records build_scene_buffer_cl(const std::vector<Shape*>& objects) {
         put_tup(R.objs, b + 384, s->material.color);
         put_tup(R.objs, b + 416, s->material.emission);
         put(R.objs, b + 448, s->material.refractive_index);
+        const Material& m = s->material;  // texture fields (scene.go:31-43)
+        if (m.textured) {
+            R.objs[b + 844] = 1;
+            R.objs[b + 845] = m.texture_id;
+            put(R.objs, b + 488, m.texture_scale_x);
+            put(R.objs, b + 496, m.texture_scale_y);
+        }
+        if (m.textured_nm) {
+            R.objs[b + 846] = 1;
+            R.objs[b + 847] = m.texture_id_nm;
+            put(R.objs, b + 504, m.texture_scale_x_nm);
+            put(R.objs, b + 512, m.texture_scale_y_nm);
+        }
+        R.objs[b + 848] = m.is_env_map ? 1 : 0;
         for (int c = 0; c < 64; c++) put(R.objs, b + 588 + 4 * (size_t)c, (int32_t)-1);
         int64_t type = 999;
         if (s->kind == GROUP) {

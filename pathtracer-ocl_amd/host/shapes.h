@@ -17,11 +17,14 @@ namespace ptmi_host {
 
 constexpr double kInf = HUGE_VAL;
 
-struct Material {  // material.Material (material/material.go:7-21); textures are not restated
+struct Material {  // material.Material (material/material.go:7-21)
     Tup color = tuple3(1, 1, 1);
     Tup emission = tuple3(0, 0, 0);
     double refractive_index = 1.0;
     double reflectivity = 0.0;
+    bool textured = false, textured_nm = false, is_env_map = false;
+    uint8_t texture_id = 0, texture_id_nm = 0;
+    double texture_scale_x = 0.0, texture_scale_y = 0.0, texture_scale_x_nm = 0.0, texture_scale_y_nm = 0.0;
 };
 inline Material new_material(Tup c, Tup e, double ri, double refl = 0.0) {
     Material m;

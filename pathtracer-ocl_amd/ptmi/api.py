@@ -18,6 +18,7 @@ import os
 import numpy as np
 
 from . import _runtime, layout
+from .textures import TextureSet
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTMI_LIB", os.path.join(_HERE, "..", "build", "libptmi.so"))
@@ -26,7 +27,7 @@ PTMI_OK, PTMI_ERR_ARG, PTMI_ERR_DEVICE, PTMI_ERR_HIP, PTMI_ERR_UNSUPPORTED, PTMI
 
 EXPORTS = ("ptmi_trace", "ptmi_device_count", "ptmi_device_name", "ptmi_scene_create", "ptmi_scene_destroy",
            "ptmi_scene_size", "ptmi_scene_render", "ptmi_finalize", "ptmi_fill_seeds", "ptmi_build_info",
-           "ptmi_scene_set_timing", "ptmi_scene_kernel_time", "ptmi_trace_multi")
+           "ptmi_scene_set_timing", "ptmi_scene_kernel_time", "ptmi_trace_multi", "ptmi_scene_create_textured")
 
 
 class PtmiError(RuntimeError):
@@ -61,6 +62,8 @@ def load_library(path=None):
     lib.ptmi_device_name.argtypes = [i32, cp, sz]
     lib.ptmi_scene_create.restype = i32
     lib.ptmi_scene_create.argtypes = [i32, vp, u32, vp, u32, vp, u32, vp, ctypes.POINTER(vp), cp, sz]
+    lib.ptmi_scene_create_textured.restype = i32
+    lib.ptmi_scene_create_textured.argtypes = [i32, vp, u32, vp, u32, vp, u32, vp, vp, ctypes.POINTER(vp), cp, sz]
     lib.ptmi_scene_destroy.restype = None
     lib.ptmi_scene_destroy.argtypes = [vp]
     lib.ptmi_scene_size.restype = i32
@@ -120,10 +123,11 @@ def Trace(objects, triangles, groups, deviceIndex, samples, camera, textures=Non
     """Drop-in for ocl.Trace (ocltracer.go:98-100).  Returns float64 RGBA, len W*H*4.
 
     ``seeds``: W*H per-pixel seeds (the Go side's rand.Float64() per pixel); None
-    lets the library generate them from ``seed_stream``.
+    lets the library generate them from ``seed_stream``.  ``textures`` /
+    ``sphereTextures`` / ``cubeTextures``: lists of H x W x 4 uint8 NRGBA images
+    (ptmi/textures.py), or None.
     """
-    if textures or sphereTextures or cubeTextures:
-        raise PtmiError(PTMI_ERR_UNSUPPORTED, "texture arrays are not supported by this build")
+    tex = TextureSet(textures, sphereTextures, cubeTextures)
     lib = load_library()
     objects, triangles, groups, camera = _records(objects, triangles, groups, camera)
     w, h = int(camera["width"][0]), int(camera["height"][0])
@@ -134,7 +138,7 @@ def Trace(objects, triangles, groups, deviceIndex, samples, camera, textures=Non
     out = np.empty(w * h * 4, dtype=np.float64)
     err = ctypes.create_string_buffer(1024)
     rc = lib.ptmi_trace(_ptr(objects), len(objects), _ptr(triangles), len(triangles), _ptr(groups), len(groups),
-                        int(deviceIndex), int(samples), _ptr(camera), _ptr(seeds), int(seed_stream), None,
+                        int(deviceIndex), int(samples), _ptr(camera), _ptr(seeds), int(seed_stream), tex.pointer(),
                         out.ctypes.data_as(ctypes.c_void_p), err, len(err))
     _check(rc, err)
     return out
@@ -143,14 +147,16 @@ def Trace(objects, triangles, groups, deviceIndex, samples, camera, textures=Non
 class Scene:
     """A scene resident on one device (ptmi_scene_*)."""
 
-    def __init__(self, device_index, objects, triangles, groups, camera):
+    def __init__(self, device_index, objects, triangles, groups, camera, textures=None, sphereTextures=None,
+                 cubeTextures=None):
         self._lib = load_library()
         objects, triangles, groups, camera = _records(objects, triangles, groups, camera)
+        tex = TextureSet(textures, sphereTextures, cubeTextures)
         handle = ctypes.c_void_p()
         err = ctypes.create_string_buffer(1024)
-        rc = self._lib.ptmi_scene_create(int(device_index), _ptr(objects), len(objects), _ptr(triangles),
-                                         len(triangles), _ptr(groups), len(groups), _ptr(camera),
-                                         ctypes.byref(handle), err, len(err))
+        rc = self._lib.ptmi_scene_create_textured(int(device_index), _ptr(objects), len(objects), _ptr(triangles),
+                                                  len(triangles), _ptr(groups), len(groups), _ptr(camera),
+                                                  tex.pointer(), ctypes.byref(handle), err, len(err))
         _check(rc, err)
         self._h = handle
         w, h = ctypes.c_uint32(), ctypes.c_uint32()

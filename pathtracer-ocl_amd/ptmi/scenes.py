@@ -372,6 +372,251 @@ def transparent_teapot_scene(width, height, aperture=0.0, focal_length=0.0, obj_
     return Scene(cam, [light, floor, ceil, left, right, back, lsp, rsp, group])
 
 
+def _textured(m, tid, sx=0.0, sy=0.0, nm=None):
+    """Material.Textured / TextureID / TextureScaleX/Y (+ the NM set when nm = (id, sx, sy))."""
+    m.textured = True
+    m.texture_id = tid
+    m.texture_scale_x = float(sx)
+    m.texture_scale_y = float(sy)
+    if nm is not None:
+        m.textured_nm = True
+        m.texture_id_nm, m.texture_scale_x_nm, m.texture_scale_y_nm = nm[0], float(nm[1]), float(nm[2])
+    return m
+
+
+# Texture lists of the textured scenes: (name, width, height) of each image the Go
+# scene loads with LoadImage (scene.go:30-56); the files are not in the reference
+# checkout, so callers supply pixels of these shapes (tests/textures_synth.py).
+TEXTURE_ASSETS = {
+    "textures": {"textures": ["concrete_squares.png", "seamless-cobblestone-texture.jpg", "floor_boards.png",
+                              "concrete_squares_nm2.png"],
+                 "sphereTextures": ["planet.png", "jupiter2_6k_contrast.png"]},
+    "envmap": {"sphereTextures": ["alps_field_8k.png"]},
+    "cubemap": {"cubeTextures": ["shrine_cubemap.jpeg"]},
+}
+
+
+def textured_planets_scene(width, height, aperture=0.0, focal_length=0.0):
+    """TexturedPlanetsScene (scenes/texturedplanets.go:13-135): textured walls (three
+    with the normal map, texture 3), floor, ceiling and two sphere-mapped planets."""
+    cam = _std_camera(width, height, aperture, focal_length)
+    left = shapes.Plane()
+    left.set_transform(geom.translate(-.6, 0, 0))
+    left.set_transform(geom.rotate_x(math.pi))
+    left.set_transform(geom.rotate_z(PI_OVER_2))
+    left.set_transform(geom.rotate_y(PI_OVER_2))
+    left.set_material(_textured(shapes.new_diffuse(0.75, 0.25, 0.25), 0, 1.0, 1.0, nm=(3, 1.0, 1.0)))
+    right = shapes.Plane()
+    right.set_transform(geom.translate(.6, 0, 0))
+    right.set_transform(geom.rotate_z(PI_OVER_2))
+    right.set_transform(geom.rotate_y(PI_OVER_2))
+    right.set_material(_textured(shapes.new_diffuse(0.25, 0.25, 0.75), 0, 1.0, 1.0, nm=(3, 1.0, 1.0)))
+    floor = shapes.Plane()
+    floor.set_transform(geom.translate(0, -.4, 0))
+    floor.set_material(_textured(shapes.new_diffuse(0.9, 0.8, 0.7), 1, 0.25, 0.25))
+    ceil = shapes.Plane()
+    ceil.set_transform(geom.translate(0, .4, 0))
+    ceil.set_material(_textured(shapes.new_diffuse(0.9, 0.8, 0.7), 2, 1.0, 1.0))
+    back = shapes.Plane()
+    back.set_transform(geom.translate(0, 0, .4))
+    back.set_transform(geom.rotate_x(PI_OVER_2))
+    back.set_material(_textured(shapes.new_diffuse(0.9, 0.8, 0.7), 0, 1.0, 1.0, nm=(3, 1.0, 1.0)))
+    lsp = shapes.Sphere()
+    lsp.set_transform(geom.translate(-0.3, -0.1, -0.25))
+    lsp.set_transform(geom.scale(0.2, 0.2, 0.2))
+    lsp.set_material(_textured(shapes.new_diffuse(0.9, 0.8, 0.7), 1))
+    rsp = shapes.Sphere()
+    rsp.set_transform(geom.translate(0.2, 0, -0.3))
+    rsp.set_transform(geom.rotate_y(math.pi))
+    rsp.set_transform(geom.scale(0.25, 0.25, 0.25))
+    rsp.set_material(_textured(shapes.new_diffuse(0.9, 0.8, 0.7), 0))
+    light = shapes.new_light_bulb()
+    light.emission = geom.color(10, 10, 10)
+    l1 = shapes.Sphere()
+    l1.set_transform(geom.translate(0, .395, -.9))
+    l1.set_transform(geom.scale(0.283, 0.01, 0.283))
+    l1.set_material(light)
+    l2 = shapes.Sphere()
+    l2.set_transform(geom.translate(0, 0, -1.7))
+    l2.set_transform(geom.scale(0.283, 0.283, 0.01))
+    l2.set_material(light)
+    return Scene(cam, [l1, l2, floor, ceil, left, right, back, lsp, rsp])
+
+
+def _sky_material(env_map=False):
+    m = _textured(shapes.new_default_material(), 0, 1.0, 1.0)
+    m.emission = geom.color(1, 1, 1)
+    m.is_env_map = env_map
+    return m
+
+
+def envmap_scene(width, height, aperture=0.0, focal_length=0.0):
+    """EnvironmentMap (scenes/envmap.go:13-72): a mirror sphere inside an emissive,
+    sphere-mapped sky sphere (the scene list holds only those two)."""
+    cam = Camera(width, height, PI_OVER_3, geom.point(0, 0.1, -1.5), geom.point(0, 0.15, 0))
+    cam.focal_length, cam.aperture = float(focal_length), float(aperture)
+    rsp = _sphere((0, -0.14, -0.30), 0.16, shapes.new_mirror())
+    sky = shapes.Sphere()
+    sky.set_transform(geom.scale(5, 5, 5))
+    sky.set_material(_sky_material())
+    return Scene(cam, [rsp, sky])
+
+
+def _cubemap_camera(width, height, aperture, focal_length):
+    cam = Camera(width, height, PI_OVER_3, geom.point(0, 0.3, -2.7), geom.point(0, 0.45, 0))
+    cam.focal_length, cam.aperture = float(focal_length), float(aperture)
+    return cam
+
+
+def cubemap_scene(width, height, aperture=0.0, focal_length=0.0):
+    """EnvironmentCubeMap (scenes/cubemap.go:15-94): light, mirror sphere, an
+    emissive cube-mapped sky cube and the BVH gopher (Divide 60)."""
+    shapes.reset_subgroup_counter()
+    cam = _cubemap_camera(width, height, aperture, focal_length)
+    rsp = _sphere((.2, 1, 2), 0.26, shapes.new_mirror())
+    light = shapes.new_light_bulb()
+    light.emission = geom.color(19.5, 19.5, 19.5)
+    lsrc = _sphere((1.1, 1, -4), 0.7, light)
+    sky = shapes.Cube()
+    sky.set_transform(geom.translate(0, 0, 0))
+    sky.set_transform(geom.scale(5, 5, 5))
+    sky.set_material(_sky_material(env_map=True))
+    group = _load_obj("gopher.obj").to_group()
+    group.bounds()
+    group.set_transform(geom.translate(-.7, -0.15, 0.2))
+    group.set_transform(geom.rotate_z(-PI_OVER_2))
+    group.set_transform(geom.rotate_x(-PI_OVER_4))
+    group.set_transform(geom.scale(0.4, 0.4, 0.4))
+    silver = shapes.new_diffuse(0.75, 0.75, 0.75)
+    silver.reflectivity = 0.0
+    group.set_material(silver)
+    shapes.divide(group, 60)
+    group.bounds()
+    return Scene(cam, [lsrc, rsp, sky, group])
+
+
+def _cube(t, s, material, rots=()):
+    c = shapes.Cube()
+    c.set_transform(geom.translate(*t))
+    for r in rots:
+        c.set_transform(r)
+    c.set_transform(geom.scale(*s))
+    c.set_material(material)
+    return c
+
+
+def gopher_window_scene(width, height, aperture=0.0, focal_length=0.0):
+    """GopherWindowScene (scenes/gopher-with-window.go:15-140): the gopher box lit
+    through an emissive window cube with four border cubes."""
+    shapes.reset_subgroup_counter()
+    cam = _std_camera(width, height, aperture, focal_length)
+    left, right, floor, ceil, back, front = _walls(back_z=1.4)
+    window = shapes.new_diffuse(0.75, 0.75, 1)
+    window.emission = geom.color(24, 24, 24)
+    ry, rx = geom.rotate_y(PI_OVER_2), geom.rotate_x(PI_OVER_2)
+    cube = _cube((0.6, .1, 0), (0.1, 0.16, 0.002), window, (ry,))
+    rb = _cube((0.6, .1, -0.1), (0.01, 0.16, 0.02), shapes.new_diffuse(0.95, 0.95, 1), (ry,))
+    lb = _cube((0.6, .1, 0.1), (0.01, 0.16, 0.02), shapes.new_diffuse(0.95, 0.95, 1), (ry,))
+    bb = _cube((0.6, -.06, 0.0), (0.01, 0.11, 0.04), shapes.new_diffuse(0.95, 0.95, 1), (rx, ry))
+    tb = _cube((0.6, .26, 0.0), (0.01, 0.11, 0.03), shapes.new_diffuse(0.95, 0.95, 1), (rx, ry))
+    csp = _sphere((0, -0.28, -0.3), 0.12, shapes.new_diffuse(0.9, 0.8, 0.7))
+    half_mirror = shapes.new_mirror()
+    half_mirror.reflectivity = 0.8
+    half_mirror.color = geom.color(0.97, 0.97, 0.843)
+    rsp = _sphere((0.28, -0.24, 0.15), 0.16, half_mirror)
+    objects = [floor, ceil, left, right, back, cube, lb, rb, bb, tb, front, csp, rsp]
+    group = _load_obj("gopher.obj").to_group()
+    group.bounds()
+    group.set_transform(geom.translate(-.4, -0.15, 0.2))
+    group.set_transform(geom.rotate_z(-PI_OVER_2))
+    group.set_transform(geom.rotate_x(-PI_OVER_4))
+    group.set_transform(geom.scale(0.2, 0.2, 0.2))
+    silver = shapes.new_diffuse(0.75, 0.75, 0.75)
+    silver.reflectivity = 0.2
+    group.set_material(silver)
+    shapes.divide(group, 60)
+    group.bounds()
+    objects.append(group)
+    light = shapes.new_light_bulb()
+    light.emission = geom.color(9, 8, 6)
+    lsrc = shapes.Sphere()
+    lsrc.set_transform(geom.translate(0, 1.36, 0))
+    lsrc.set_material(light)
+    objects.append(lsrc)
+    return Scene(cam, objects)
+
+
+def christian_scene(width, height, aperture=0.0, focal_length=0.0, obj_path=None):
+    """ChristianScene (scenes/christian.go:14-190): the teapot box with four small
+    lights under open reflective cylinder covers and a mirror-like sphere."""
+    shapes.reset_subgroup_counter()
+    cam = _std_camera(width, height, aperture, focal_length)
+    left, right, floor, ceil, back, _front = _walls()
+    lsp = _sphere((-0.35, -0.28, -0.15), 0.12, shapes.new_diffuse(0.9, 0.9, 0.9))
+    lsp.material.reflectivity = 0.99
+    model = _load_obj("teapot.obj") if obj_path is None else objparser.parse_obj(open(obj_path).read())
+    group = model.to_group()
+    objparser.compute_vertex_normals(list(group.children[0].children))
+    group.bounds()
+    group.set_transform(geom.translate(0, -0.4, 0))
+    group.set_transform(geom.scale(0.07, 0.07, 0.07))
+    silver = shapes.new_diffuse(0.75, 0.75, 0.75)
+    silver.reflectivity = 0.2
+    group.set_material(silver)
+    shapes.divide(group, 50)
+    group.bounds()
+    light = shapes.new_light_bulb()
+    light.emission = geom.color(90, 80, 60)
+    cover_m = shapes.new_diffuse(0.8, 0.8, 0.8)
+    cover_m.reflectivity = 0.95
+
+    def lamp(x):
+        return _sphere((x, .3, 0), 0.03, light)
+
+    def cover(x):
+        c = shapes.Cylinder(0, 1, False)
+        c.set_transform(geom.translate(x, .295, 0))
+        c.set_transform(geom.scale(0.06, 0.4, 0.06))
+        c.set_material(cover_m)
+        return c
+
+    return Scene(cam, [lamp(-0.3), lamp(-0.1), lamp(0.1), lamp(0.3), cover(-0.3), cover(-0.1), cover(0.1),
+                       cover(0.3), floor, ceil, left, right, back, group, lsp])
+
+
+def glass_scene(width, height, aperture=0.0, focal_length=0.0, obj_path=None):
+    """GlassScene (scenes/transparent_glass.go:15-146).  Its mesh, assets/glass.obj,
+    is not shipped with the reference (its own objparser test fails on it), so
+    without ``obj_path`` this raises as the Go os.ReadFile panic does."""
+    shapes.reset_subgroup_counter()
+    cam = _std_camera(width, height, aperture, focal_length)
+    left, right, floor, ceil, back, front = _labelled(_walls(.6), _WALL_LABELS)
+    lsp = _sphere((-0.2, -0.28, 0.25), 0.12, shapes.new_mirror())
+    rsp = _sphere((0.25, -0.28, 0.25), 0.12, shapes.new_glass())
+    _labelled((lsp, rsp), ("left_spr", "right_spr"))
+    mtrl = shapes.new_glass()
+    mtrl.reflectivity = 0.0
+    model = _load_obj("glass.obj") if obj_path is None else objparser.parse_obj(open(obj_path).read())
+    group = model.to_group()
+    objparser.compute_vertex_normals(list(group.children[0].children) + list(group.children[1].children))
+    group.bounds()
+    group.set_transform(geom.translate(-0.3, -0.395, -0.2))
+    group.set_transform(geom.scale(0.03, 0.03, 0.03))
+    group.set_material(mtrl)
+    shapes.divide(group, 50)
+    group.bounds()
+    group.label = "glass   "
+    lights = [_cube_light((-0.25 + float(i) * 0.5, .4, -0.25 + float(j) * 0.5), (0.15, 0.001, 0.15),
+                          geom.color(10, 10, 10)) for i in range(2) for j in range(2)]
+    _labelled(lights, ["light %d-%d" % (i, j) for i in range(2) for j in range(2)])
+    return Scene(cam, [floor, ceil, left, right, back, front, lsp, rsp, group] + lights)
+
+
+# Scene cameras other than _std_camera (records of mesh scenes are pre-built; only
+# the camera is rebuilt per W/H).
+CAMERAS = {"cubemap": _cubemap_camera}
+
+
 SCENES = {
     "reference": reference_scene,
     "reflection": reflection_scene,
@@ -382,4 +627,10 @@ SCENES = {
     "teapot": teapot_scene,
     "gopher": gopher_scene,
     "default": ocl_scene,
+    "textures": textured_planets_scene,
+    "envmap": envmap_scene,
+    "cubemap": cubemap_scene,
+    "gopher-window": gopher_window_scene,
+    "christian": christian_scene,
+    "glass": glass_scene,
 }

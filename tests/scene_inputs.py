@@ -16,15 +16,20 @@ sys.path.insert(0, os.path.join(HERE, "..", "pathtracer-ocl_amd"))
 from ptmi import layout, scenes  # noqa: E402
 
 _cache = {}
-MESH_SCENES = ("teapot", "gopher", "transparent_teapot")  # records from tests/golden/scene_<name>.npz
+# records from tests/golden/scene_<name>.npz (cubemap / gopher-window / christian
+# store only their objects and reuse their base mesh's triangles and groups)
+MESH_SCENES = ("teapot", "gopher", "transparent_teapot", "cubemap", "gopher-window", "christian")
 
 
 def _load_mesh_scene(name):
     if name not in _cache:
-        z = np.load(os.path.join(HERE, "golden", "scene_%s.npz" % name))
-        _cache[name] = (z["objects"].view(layout.OBJECT_DTYPE).copy(),
-                        z["triangles"].view(layout.TRIANGLE_DTYPE).copy(),
-                        z["groups"].view(layout.GROUP_DTYPE).copy())
+        z = np.load(os.path.join(HERE, "golden", "scene_%s.npz" % name.replace("-", "_")))
+        if "mesh" in z.files:
+            _, tris, grps = _load_mesh_scene(str(z["mesh"]))
+        else:
+            tris = z["triangles"].view(layout.TRIANGLE_DTYPE).copy()
+            grps = z["groups"].view(layout.GROUP_DTYPE).copy()
+        _cache[name] = (z["objects"].view(layout.OBJECT_DTYPE).copy(), tris, grps)
     return _cache[name]
 
 
@@ -32,7 +37,7 @@ def scene_inputs(name, width, height, aperture=0.0, focal_length=0.0):
     """-> (objects, triangles, groups, camera) records (triangles/groups may be empty)."""
     if name in MESH_SCENES:
         objs, tris, grps = _load_mesh_scene(name)
-        cam = scenes._std_camera(width, height, aperture, focal_length)
+        cam = scenes.CAMERAS.get(name, scenes._std_camera)(width, height, aperture, focal_length)
         return objs, tris, grps, layout.camera_record(cam)
     sc = scenes.SCENES[name](width, height, aperture, focal_length)
     objs, tris, grps = layout.build_scene_buffer_cl(sc.objects)

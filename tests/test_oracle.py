@@ -86,10 +86,16 @@ def test_dof_sample_zero_is_black():
     assert np.all(s0.reshape(-1, 4)[:, :3] == 0.0)
 
 
-def test_textured_objects_rejected():
-    objs, tris, grps, cam = scene_inputs("reference", 8, 8)
-    objs = objs.copy()
-    objs["is_textured"][1] = 1
+def test_textured_object_without_textures_is_black():
+    """A textured object with no texture arrays samples the reference's all-zero
+    fake image (ocltracer.go:249-251): its bounce colour becomes (0, 0, 0)."""
+    objs, tris, grps, cam = scene_inputs("reference", 16, 12)
     tris, grps = layout.pad_empty(tris, grps)
-    with pytest.raises(RuntimeError):
-        pyoracle.cpu_trace(objs, tris, grps, cam, 1, layout.seeds_go_float64(64))
+    seeds = layout.seeds_go_float64(16 * 12, 5)
+    tex = objs.copy()
+    tex["is_textured"][1] = 1  # the floor plane
+    black = objs.copy()
+    black["color"][1][:3] = 0.0
+    a = pyoracle.cpu_trace(tex, tris, grps, cam, 2, seeds)
+    b = pyoracle.cpu_trace(black, tris, grps, cam, 2, seeds)
+    assert np.array_equal(a, b)
