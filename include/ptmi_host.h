@@ -22,6 +22,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "ptmi.h" /* ptmi_textures, PTMI_ERR_* */
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -54,6 +56,23 @@ int ptmi_host_write_png(const char* path, const double* rgba, int width, int hei
 /* .raw image (raw/writer.go:11-35): big-endian int32 1, 0, width, height, then
  * width*height big-endian float32 (R, G, B) triples; alpha is dropped. */
 int ptmi_host_write_raw(const char* path, const double* rgba, int width, int height, char* err, size_t err_len);
+
+/* LoadImage (internal/app/scenes/scene.go:30-56): a PNG file decoded as Go's
+ * image/png does, converted to NRGBA8 as draw.Draw(NRGBA, Src) does; *nrgba gets
+ * width*height*4 bytes (free with ptmi_host_free_image).  .jpg/.jpeg: image/jpeg is
+ * not restated -- a PNG with the same stem is read instead when present, else error. */
+int ptmi_host_load_image(const char* path, uint8_t** nrgba, uint32_t* width, uint32_t* height, char* err,
+                         size_t err_len);
+void ptmi_host_free_image(uint8_t* nrgba);
+
+/* The texture arrays a named scene passes to ocl.Trace (Scene.Textures /
+ * SphereTextures / CubeTextures) loaded from `assets_dir` and packed as
+ * prepareTextures does (ocltracer.go:228-254): per list, width/height of its first
+ * image and the NRGBA bytes of all its images concatenated.  Scenes without
+ * textures get all counts 0.  Free with ptmi_host_free_textures. */
+int ptmi_host_load_scene_textures(const char* name, const char* assets_dir, ptmi_textures* out, char* err,
+                                  size_t err_len);
+void ptmi_host_free_textures(ptmi_textures* t);
 
 #ifdef __cplusplus
 }

@@ -120,6 +120,13 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "scene build failed (%d): %s\n", rc, err);
         return 1;
     }
+    ptmi_textures tex;  // the scene's texture arrays (texturedplanets / envmap / cubemap)
+    if ((rc = ptmi_host_load_scene_textures(scene.c_str(), c.assets.c_str(), &tex, err, sizeof(err)))) {
+        ptmi_host_free_records(&r);
+        std::fprintf(stderr, "%s\n", err);  // the reference: LoadImage panics
+        return 1;
+    }
+    const bool textured = tex.count[0] || tex.count[1] || tex.count[2];
     const auto t1 = std::chrono::steady_clock::now();
     const size_t n = (size_t)c.width * c.height;
     std::vector<double> out(n * 4);
@@ -127,15 +134,17 @@ int main(int argc, char** argv) {
         c.have_seed ? c.seed : (uint64_t)std::chrono::system_clock::now().time_since_epoch().count();
     if (c.gpus == 1) {
         rc = ptmi_trace(r.objects, r.n_obj, r.triangles, r.n_tri, r.groups, r.n_grp, c.device_index,
-                        (uint32_t)c.samples, r.camera, nullptr, stream, nullptr, out.data(), err, sizeof(err));
+                        (uint32_t)c.samples, r.camera, nullptr, stream, textured ? &tex : nullptr, out.data(), err,
+                        sizeof(err));
     } else {
         std::vector<int> devs(c.gpus);
         for (int d = 0; d < c.gpus; d++) devs[d] = d;
         rc = ptmi_trace_multi(r.objects, r.n_obj, r.triangles, r.n_tri, r.groups, r.n_grp, devs.data(),
                               (uint32_t)c.gpus, c.split == "tile" ? 1 : 0, (uint32_t)c.samples, r.camera, nullptr,
-                              stream, nullptr, out.data(), err, sizeof(err));
+                              stream, textured ? &tex : nullptr, out.data(), err, sizeof(err));
     }
     ptmi_host_free_records(&r);
+    ptmi_host_free_textures(&tex);
     if (rc) {
         std::fprintf(stderr, "ptmi_trace failed (%d): %s\n", rc, err);  // the reference: logrus.Fatalf
         return 1;

@@ -53,3 +53,30 @@ def test_cli_multi_device_flags(tmp_path):
                        timeout=300)
     assert r.returncode == 0, r.stderr
     assert os.path.getsize(png) > 0
+
+
+@pytest.mark.parametrize("scene,w,h,spp", [("textures", 48, 32, 4), ("envmap", 40, 30, 4)])
+def test_cli_textured_scene(tmp_path, scene, w, h, spp):
+    """Textured scenes end to end: images loaded from --assets (PNG stand-ins of
+    the reference's missing assets, the .jpg one as a same-stem .png), packed as
+    prepareTextures does and sampled on the GPU == api.Trace with the same arrays."""
+    from ptmi import scenes
+    from tests import textures_synth
+    from tests.test_host_images import write_png
+    tex = textures_synth.scene_textures(scene)
+    for k, key in enumerate(("textures", "sphereTextures", "cubeTextures")):
+        for name, img in zip(scenes.TEXTURE_ASSETS[scene].get(key, []), tex[k] or []):
+            stem = name.rsplit(".", 1)[0]
+            write_png(tmp_path / (stem + ".png"), img.astype(np.int64), 6, 8)
+    png = tmp_path / "o.png"
+    cmd = [PT, "--scene", scene, "--width", str(w), "--height", str(h), "--samples", str(spp), "--seed", "77",
+           "--assets", str(tmp_path), "--out", str(png)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    objs, tris, grps, cam = scene_inputs(scene, w, h)
+    ref = api.Trace(objs, tris, grps, 0, spp, cam, *tex, seed_stream=77).reshape(h, w, 4)
+    assert np.array_equal(_read_png(str(png))[..., :3], _clamp(ref[..., :3]))
+    # without the images the CLI fails loudly, as LoadImage panics
+    r = subprocess.run(cmd[:-4] + ["--assets", str(tmp_path / "none"), "--out", str(png)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode != 0 and "cannot read" in r.stderr
