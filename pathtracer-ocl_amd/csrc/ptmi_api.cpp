@@ -416,6 +416,7 @@ int ptmi_scene_create_textured(int device_index, const void* objects, uint32_t n
     s->dev.n_obj = (uint32_t)objs.size();
     s->dev.n_list = n_obj;
     s->dev.n_nodes = n_grp;
+    s->dev.n_nodes4 = (int32_t)index.nodes.size();
     s->dev.n_tri = n_tri;
     s->dev.cam = cam;
     hipDeviceProp_t p;

@@ -312,8 +312,10 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
         return n.left < 0 ? leaf_code(leaf_first[bi], n.count) : -2;  // -2: inner, resolved below
     };
     // Collapse the binary tree to 4-wide nodes (children = grandchildren of
-    // inner children), emitted in creation order.
-    std::vector<std::pair<int, int>> work;  // (binary node, Node4 slot)
+    // inner children), emitted breadth first: the top levels of the first
+    // object's index are the first Node4s, which the kernel stages in LDS.
+    std::vector<std::pair<int, int>> work;  // (binary node, Node4 slot), a FIFO
+    size_t work_head = 0;
     auto emit = [&](int bi) -> int32_t {
         if (B.nodes[bi].left < 0) return code_of(bi);
         const int32_t slot = (int32_t)out.nodes.size();
@@ -322,9 +324,8 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
         return slot;
     };
     *entry = emit(broot);
-    while (!work.empty()) {
-        auto [bi, slot] = work.back();
-        work.pop_back();
+    while (work_head < work.size()) {
+        auto [bi, slot] = work[work_head++];
         int kids[4], nk = 0;
         for (int c : {B.nodes[bi].left, B.nodes[bi].right}) {
             if (B.nodes[c].left >= 0) {

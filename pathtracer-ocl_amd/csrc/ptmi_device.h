@@ -132,7 +132,7 @@ struct DevScene {
     const PlaneRec* planes;      // all planes
     const SphereRec* spheres;    // scale+translate spheres (the rest: DevObject path)
     int32_t n_spheres_st;
-    int32_t pad1;
+    int32_t n_nodes4;  // Node4 count (the first min(n, kLdsNodes) are staged in LDS)
     const int32_t* roots;  // concatenated group roots of all type-4 objects
     const RootRec* root_rec;  // per roots[] slot
     const DevNode* nodes;

@@ -384,6 +384,10 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 
 }
 
 static constexpr int kStack = 24;  // per-lane LDS traversal stack (3 pushes x BVH4 depth <= 7, ptmi_bvh.cpp)
+#ifndef PTMI_LDS_NODES
+#define PTMI_LDS_NODES 120  // Node4s staged in LDS per workgroup: 4 full BVH4 levels + 35 (13.1 KB)
+#endif
+static constexpr int kLdsNodes = PTMI_LDS_NODES;
 
 // The reference's gate for one triangle: every reference node on the path from
 // the walked root to the triangle's node passes intersectRayWithBox
@@ -418,8 +422,8 @@ __device__ __forceinline__ bool cull_box(d4 o, d4 r, double mnx, double mny, dou
 // not depend on the visiting order or the widened boxes (every triangle that
 // can produce a winning t is reached); ties resolve through better_tri.
 template <bool kVerify>
-__device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const RootRec& R, int slot,
-                                           int key, d4 o, d4 d, Hit& h, int& vchain) {
+__device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes,
+                                           const RootRec& R, int slot, int key, d4 o, d4 d, Hit& h, int& vchain) {
     // FP32 slab tests.  With of = (float)o, rf = (float)(1/d) (|rf| clamped to
     // 1e30) and t' = fma(b, rf, -RN(of*rf)), the computed slab bound differs from
     // the exact (b - o)/d by at most 2^-23 |r| (|b| + 2|o|) (FP32 roundings of o,
@@ -445,7 +449,8 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
     while (true) {
         if (cur >= 0) {
             PTMI_COUNT(1);
-            const Node4& N = S.nodes4[cur];
+            // the first kLdsNodes Node4s (the top levels, ptmi_bvh.cpp) are staged in LDS
+            const Node4& N = cur < kLdsNodes ? lds_nodes[cur] : S.nodes4[cur];
             const double limd = h.t + prune_margin(h.t);
             const float lim = (float)limd * (1.0f + 0x1p-22f) + 0x1p-100f;  // >= limd
             float k[4];
@@ -633,7 +638,8 @@ __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd
 // each improving candidate (exact by construction, slower: the check runs
 // inside the divergent walk loop).
 template <bool A, bool kVerify>
-__device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
+__device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes, d4 ro,
+                                                 d4 rd, Hit& h) {
 #if defined(PTMI_EXP) && (PTMI_EXP & 1)
     return;
 #endif
@@ -653,7 +659,7 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restr
             if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
                          R.hull_mx[2], h.t + prune_margin(h.t), tn))
                 continue;
-            walk_index<kVerify>(S, stk, R, j, ob.key, o, d, h, vchain);
+            walk_index<kVerify>(S, stk, lds_nodes, R, j, ob.key, o, d, h, vchain);
         }
     }
 }
@@ -666,9 +672,10 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restr
 // tests/adversarial.py) are this ray's walks redone with eager checks.  All
 // lanes verify together after the loop instead of one by one inside it.
 template <bool A>
-__device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
+__device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes, d4 ro, d4 rd,
+                                            Hit& h) {
     const Hit h0 = h;
-    group_walks_impl<A, false>(S, stk, ro, rd, h);
+    group_walks_impl<A, false>(S, stk, lds_nodes, ro, rd, h);
     if (h.tri >= 0) {  // the winner is a triangle (h0 holds primitives only)
         PTMI_COUNT(4);
         const DevObject& ob = S.objs[h.obj];
@@ -678,7 +685,7 @@ __device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__
         if (!verify_chain(S, h.chain, o, d)) {
             PTMI_COUNT(11);  // (stats build: eager re-walks)
             h = h0;
-            group_walks_impl<A, true>(S, stk, ro, rd, h);
+            group_walks_impl<A, true>(S, stk, lds_nodes, ro, rd, h);
         }
 #endif
     }
@@ -1099,6 +1106,16 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
                                                     uint32_t chunk_len, uint32_t tile_stride, uint32_t tile_offset,
                                                     const double* __restrict__ seeds, const double* __restrict__ sunf,
                                                     double* __restrict__ out) {
+    // Top levels of the traversal index in LDS (group scenes), staged by the whole
+    // workgroup before any wave can leave.  Entries past n_nodes4 are never read.
+    __shared__ float4 node_lds4[(FL & F_GROUPS) ? (kLdsNodes > 0 ? kLdsNodes : 1) * 7 : 1];
+    const Node4* node_lds = reinterpret_cast<const Node4*>(node_lds4);
+    if constexpr ((FL & F_GROUPS) != 0 && kLdsNodes > 0) {
+        const int nl = min(kLdsNodes, S.n_nodes4) * 7;
+        const float4* src = reinterpret_cast<const float4*>(S.nodes4);
+        for (int k = threadIdx.x; k < nl; k += 256) node_lds4[k] = src[k];
+        __syncthreads();
+    }
     const int W = S.cam.width, H = S.cam.height;
     const int tiles_x = (W + kTile - 1) / kTile;
     const int tiles_y = (H + kTile - 1) / kTile;
@@ -1212,7 +1229,7 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
 #endif
                 if (pending) {
                     h = hp;
-                    group_walks<A>(S, stk, P.ro, P.rd, h);
+                    group_walks<A>(S, stk, node_lds, P.ro, P.rd, h);
                     pending = false;
                     ready = true;
                 }
