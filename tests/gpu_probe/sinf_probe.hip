@@ -36,29 +36,29 @@ extern "C" int probe_sinf_all(unsigned long long* mismatches, unsigned int* firs
     unsigned long long* dm;
     unsigned int* df;
     if (hipMalloc(&dm, 8) || hipMalloc(&df, 4)) return -1;
-    hipMemset(dm, 0, 8);
-    hipMemset(df, 0xff, 4);
+    (void)hipMemset(dm, 0, 8);
+    (void)hipMemset(df, 0xff, 4);
     const uint64_t chunk = 1ull << 28;
     for (uint64_t base = 0; base < (1ull << 32); base += chunk) {
         hipLaunchKernelGGL(sinf_check, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, chunk, dm, df);
         if (hipGetLastError() != hipSuccess) return -2;
     }
     if (hipDeviceSynchronize() != hipSuccess) return -3;
-    hipMemcpy(mismatches, dm, 8, hipMemcpyDeviceToHost);
-    hipMemcpy(first_bad, df, 4, hipMemcpyDeviceToHost);
-    hipFree(dm);
-    hipFree(df);
+    (void)hipMemcpy(mismatches, dm, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(first_bad, df, 4, hipMemcpyDeviceToHost);
+    (void)hipFree(dm);
+    (void)hipFree(df);
     return 0;
 }
 
 extern "C" int probe_sinf_eval(const float* in, float* out, uint64_t n) {
     float *din, *dout;
     if (hipMalloc(&din, n * 4) || hipMalloc(&dout, n * 4)) return -1;
-    hipMemcpy(din, in, n * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(din, in, n * 4, hipMemcpyHostToDevice);
     hipLaunchKernelGGL(sinf_eval, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, din, dout, n);
     if (hipDeviceSynchronize() != hipSuccess) return -3;
-    hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost);
-    hipFree(din);
-    hipFree(dout);
+    (void)hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(din);
+    (void)hipFree(dout);
     return 0;
 }
