@@ -42,8 +42,26 @@ static constexpr double kEps = 0.0001;               // tracer.cl:4
 static constexpr double kPi = (double)3.14159265359f;  // tracer.cl:1 (a float literal)
 // Camera-ray batch refill policy (trace_kernel): refill when this many lanes
 // have an empty buffer, or this many lanes are idle waiting for a ray.
-static constexpr int kRefillNeed = 24;
-static constexpr int kRefillStarve = 6;
+// Camera-ray refill of a wave (trace_kernel): when kRefillNeed lanes have an empty
+// buffer (64: all of them), or kRefillStarve lanes sit idle without a path.  Full
+// batches amortise the camera block; measured on C2 (512 spp): 24/6 61.9 ms,
+// 40/10 61.1, 60/24 60.3, 64/24 59.7; the group scenes prefer 64/12.
+#ifndef PTMI_REFILL_NEED
+#define PTMI_REFILL_NEED 64
+#endif
+#ifndef PTMI_REFILL_STARVE
+#define PTMI_REFILL_STARVE 24
+#endif
+#ifndef PTMI_REFILL_STARVE_GROUPS
+#define PTMI_REFILL_STARVE_GROUPS 12
+#endif
+#ifndef PTMI_CAM_DEPTH
+#define PTMI_CAM_DEPTH 1  // camera rays buffered per lane (2 and 3 measured no faster on C2)
+#endif
+#ifndef PTMI_CAM_DEPTH_GROUPS
+#define PTMI_CAM_DEPTH_GROUPS 1
+#endif
+static constexpr int kRefillNeed = PTMI_REFILL_NEED;
 #ifndef PTMI_WALK_BATCH
 #define PTMI_WALK_BATCH 24
 #endif
@@ -1136,59 +1154,66 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
     const float fgi2 = (float)(seed / (double)samples);
     double cr = 0.0, cg = 0.0, cb = 0.0;
     const CamConst cc = cam_const(S.cam);
-    // Camera rays are produced in wave-wide batches into a one-deep per-lane
-    // buffer (LDS) and consumed by path regeneration: generating them at the
+    // Camera rays are produced in wave-wide batches into a kCamDepth-deep per-lane
+    // ring buffer (LDS) and consumed by path regeneration: generating them at the
     // moment each lane needs one would run the camera block (2 noise3D + the
     // transform) on nearly every bounce iteration with ~1/5 of the lanes active.
     // Per lane the samples are still traced in order n = c0, c0+1, ..., so the
     // arithmetic and the order of `colors +=` are unchanged.
-    // SoA, component c of lane t at [c * 256 + t]; affine scenes keep no w lanes.
+    // SoA, component c of slot k, lane t at [(k * kCamComp + c) * 256 + t]; affine
+    // scenes keep no w lanes.  Group scenes stay one deep (their LDS holds the
+    // traversal stacks and nodes).
     constexpr int kCamComp = A ? 6 : 8;
-    __shared__ double cam_lds[kCamComp * 256];
+    constexpr int kCamDepth = (FL & F_GROUPS) ? PTMI_CAM_DEPTH_GROUPS : PTMI_CAM_DEPTH;
+    __shared__ double cam_lds[kCamDepth * kCamComp * 256];
     const int tid = threadIdx.x;
     // Per-lane BVH traversal stacks, lane-interleaved (entry k of lane t at
     // [k * 256 + t]) so a wave's pushes and pops hit 64 consecutive dwords.
     __shared__ int stk_lds[(FL & F_GROUPS) ? kStack * 256 : 1];
     int* stk = (FL & F_GROUPS) ? stk_lds + tid : nullptr;
     uint32_t n_gen = c0;  // next sample whose camera ray is to be generated
-    uint32_t n_buf = 0, n_cur = 0;
-    bool buf = false, active = false, pending = false;
+    uint32_t n_cur = 0;
+    int nb = 0, hb = 0;   // buffered camera rays (samples n_gen - nb ...) and the head slot
+    bool active = false, pending = false;
     PathState P;
     Hit hp;
     for (;;) {
-        if (!__any(active || buf || n_gen < c1)) break;
-        const bool need = !buf && n_gen < c1;
+        if (!__any(active || nb > 0 || n_gen < c1)) break;
+        const bool need = nb < kCamDepth && n_gen < c1;
         const int n_need = __popcll(__ballot(need));
-        const int n_starve = __popcll(__ballot(need && !active));
+        const int n_starve = __popcll(__ballot(nb == 0 && !active && n_gen < c1));
+        constexpr int kRefillStarve = (FL & F_GROUPS) ? PTMI_REFILL_STARVE_GROUPS : PTMI_REFILL_STARVE;
         if (n_need >= kRefillNeed || n_starve >= kRefillStarve || (n_starve > 0 && !__any(active))) {
             if (need) {
                 d4 ro, rd;
                 ray_for_pixel<(FL & F_DOF) != 0, A>(S.cam, cc, sunf, (unsigned)px, (unsigned)py,
                                                     noise3d(fgi, (float)n_gen, fgi2), noise3d(fgi, fgi2, (float)n_gen),
                                                     (int)n_gen, ro, rd);
-                cam_lds[0 * 256 + tid] = ro.x;
-                cam_lds[1 * 256 + tid] = ro.y;
-                cam_lds[2 * 256 + tid] = ro.z;
-                cam_lds[3 * 256 + tid] = rd.x;
-                cam_lds[4 * 256 + tid] = rd.y;
-                cam_lds[5 * 256 + tid] = rd.z;
+                int slot = hb + nb;
+                if (slot >= kCamDepth) slot -= kCamDepth;
+                double* cb = cam_lds + slot * (kCamComp * 256) + tid;
+                cb[0 * 256] = ro.x;
+                cb[1 * 256] = ro.y;
+                cb[2 * 256] = ro.z;
+                cb[3 * 256] = rd.x;
+                cb[4 * 256] = rd.y;
+                cb[5 * 256] = rd.z;
                 if constexpr (!A) {
-                    cam_lds[6 * 256 + tid] = ro.w;
-                    cam_lds[7 * 256 + tid] = rd.w;
+                    cb[6 * 256] = ro.w;
+                    cb[7 * 256] = rd.w;
                 }
-                n_buf = n_gen;
                 n_gen++;
-                buf = true;
+                nb++;
             }
         }
-        if (!active && buf) {
-            const d4 cro = mk(cam_lds[0 * 256 + tid], cam_lds[1 * 256 + tid], cam_lds[2 * 256 + tid],
-                              A ? 1.0 : cam_lds[6 * 256 + tid]);
-            const d4 crd = mk(cam_lds[3 * 256 + tid], cam_lds[4 * 256 + tid], cam_lds[5 * 256 + tid],
-                              A ? 0.0 : cam_lds[7 * 256 + tid]);
+        if (!active && nb > 0) {
+            const double* cb = cam_lds + hb * (kCamComp * 256) + tid;
+            const d4 cro = mk(cb[0 * 256], cb[1 * 256], cb[2 * 256], A ? 1.0 : cb[6 * 256]);
+            const d4 crd = mk(cb[3 * 256], cb[4 * 256], cb[5 * 256], A ? 0.0 : cb[7 * 256]);
             start_path<A>(P, cro, crd);
-            n_cur = n_buf;
-            buf = false;
+            n_cur = n_gen - (uint32_t)nb;
+            hb = (hb + 1 == kCamDepth) ? 0 : hb + 1;
+            nb--;
             active = true;
         }
         // Closest hit.  Scenes with BVH groups defer the walks: a lane whose ray
