@@ -9,8 +9,8 @@ import shutil
 import sys
 
 CMDS = {"c2": "python3 bench.py --config c2 --steps 2 --warmup 1",
-        "c4": "python3 bench.py --config c4 --samples 256 --steps 1 --warmup 1 --no-cpu-baseline",
-        "c5": "python3 bench.py --config c5 --samples 256 --steps 1 --warmup 1 --no-cpu-baseline"}
+        "c4": "python3 bench.py --config c4 --samples 256 --steps 1 --warmup 1 --no-cpu-baseline --no-trace-call",
+        "c5": "python3 bench.py --config c5 --samples 256 --steps 1 --warmup 1 --no-cpu-baseline --no-trace-call"}
 
 
 def main(src, dst):
@@ -32,21 +32,28 @@ def main(src, dst):
         rf = b["roofline"]
         lines.append("  bench: value %.2f Msamples/s  kernel_ms_avg (HIP events) %.3f  achieved %.3f TF/s  frac %.4f"
                      % (b["value"], rf["kernel_ms_avg"], rf["achieved"], rf["frac"]))
+        if b.get("ptmi_trace_call"):
+            tc = b["ptmi_trace_call"]
+            lines.append("  ptmi_trace call (PCIe-inclusive, scene upload + BVH build): %.1f ms = %.2f Msamples/s"
+                         % (tc["ms"], tc["value"]))
         if b.get("cpu_baseline"):
             cb = b["cpu_baseline"]
             lines.append("  cpu_baseline: %.2f %s on %d cores (%s; %s)" % (cb["value"], cb["unit"], cb["cores"],
                                                                          cb["kind"], cb["sample"]))
         lines.append("")
-    shutil.copy(os.path.join(src, "pmc_c2.json"), os.path.join(dst, "pmc_c2.json"))
-    for k in ("fetch", "write"):
-        shutil.copy(os.path.join(src, "c2_%s" % k, "run_counter_collection.csv"),
-                    os.path.join(dst, "pmc_c2_%s.csv" % k))
-    with open(os.path.join(dst, "pmc_c2.json")) as f:
-        p = json.load(f)
-    lines.append("## c2 HBM traffic (separate --pmc passes, 1 frame): FETCH_SIZE %.1f KB (x2 gfx950 correction), "
-                 "WRITE_SIZE %.1f KB -> %.1f MB per launch" % (p["fetch_size_kb_raw_per_launch"],
-                                                             p["write_size_kb_per_launch"],
-                                                             p["hbm_bytes_per_launch"] / 1e6))
+    for cfg, what in (("c2", "1 frame, 2048 spp"), ("c4", "1 frame, 256 spp")):
+        if not os.path.exists(os.path.join(src, "pmc_%s.json" % cfg)):
+            continue
+        shutil.copy(os.path.join(src, "pmc_%s.json" % cfg), os.path.join(dst, "pmc_%s.json" % cfg))
+        for k in ("fetch", "write"):
+            shutil.copy(os.path.join(src, "%s_%s" % (cfg, k), "run_counter_collection.csv"),
+                        os.path.join(dst, "pmc_%s_%s.csv" % (cfg, k)))
+        with open(os.path.join(dst, "pmc_%s.json" % cfg)) as f:
+            p = json.load(f)
+        lines.append("## %s HBM traffic (separate --pmc passes, %s): FETCH_SIZE %.1f KB (x2 gfx950 correction), "
+                     "WRITE_SIZE %.1f KB -> %.1f MB per launch" % (cfg, what, p["fetch_size_kb_raw_per_launch"],
+                                                                 p["write_size_kb_per_launch"],
+                                                                 p["hbm_bytes_per_launch"] / 1e6))
     with open(os.path.join(dst, "SUMMARY.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
