@@ -135,6 +135,9 @@ int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, u
     cam.aperture = rd<double>(camera + 40);
     cam.focal_length = rd<double>(camera + 48);
     std::memcpy(cam.inv, camera + 56, 128);
+    for (int r = 0; r < 4; r++)  // mul (tracer.cl:369-376) of the point (0,0,0,1); no contraction (Makefile)
+        cam.origin[r] = ((cam.inv[4 * r] * 0.0 + cam.inv[4 * r + 1] * 0.0) + cam.inv[4 * r + 2] * 0.0) +
+                        cam.inv[4 * r + 3] * 1.0;
     if (cam.width <= 0 || cam.height <= 0 || (int64_t)cam.width * cam.height > (int64_t)1 << 30) {
         set_err(err, err_len, "bad camera size %dx%d", cam.width, cam.height);
         return PTMI_ERR_ARG;

@@ -107,6 +107,8 @@ struct DevCamera {
     int32_t width, height;
     double pixel_size, half_width, half_height, aperture, focal_length;
     double inv[16];
+    double origin[4];  // mul(inv, (0,0,0,1)) (tracer.cl:760), computed once on the host with the
+                       // same separately rounded IEEE arithmetic: a frame constant in kernel args
 };
 
 // Compact records for the two hottest intersection loops (read with scalar

@@ -776,40 +776,26 @@ __device__ __noinline__ void sunflower(int amount, int point, double& ox, double
     oy = r * st;
 }
 
-// Per-frame camera constants (computed once per thread from the uniform camera
-// record; exact rewrites of the reference's rayForPixel arithmetic):
-//   origin = mul(inverse, (0,0,0,1))                      -- a frame constant
-//   pixel  = mul(inverse, (hw - xo, hh - yo, -1, 1)) where m*(-1) == -m and
-//            m*1 == m exactly, so row r = ((m0 a + m1 b) + (-m2)) + m3.
-struct CamConst {
-    d4 origin;
-    double nm2[4], m3[4];
-};
-__device__ __forceinline__ CamConst cam_const(const DevCamera& cam) {
-    CamConst c;
-    c.origin = mat_mul(cam.inv, mk(0.0, 0.0, 0.0, 1.0));
-    for (int r = 0; r < 4; r++) {
-        c.nm2[r] = -cam.inv[4 * r + 2];
-        c.m3[r] = cam.inv[4 * r + 3];
-    }
-    return c;
-}
-
 // rayForPixel (tracer.cl:745-779).  With DoF the aperture offset
 // sunflower(S, 2, n) depends only on n: it is read from a per-frame table
 // (sunflower_kernel) made with the same arithmetic.
+//   origin = mul(inverse, (0,0,0,1)): a frame constant, DevCamera::origin
+//   pixel  = mul(inverse, (hw - xo, hh - yo, -1, 1)) where m*(-1) == -m and
+//            m*1 == m exactly, so row r = ((m0 a + m1 b) + (-m2)) + m3.
+// Everything uniform comes straight from the kernel arguments (scalar
+// registers); nothing per-frame is kept live in vector registers across the
+// bounce loop.
 template <bool kDof, bool A>
-__device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, const CamConst& cc, const double* __restrict__ sunf,
-                                              unsigned x, unsigned y, float rx, float ry, int sample, d4& ro,
-                                              d4& rd) {
+__device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, const double* __restrict__ sunf, unsigned x,
+                                              unsigned y, float rx, float ry, int sample, d4& ro, d4& rd) {
     double xo = cam.pixel_size * ((double)x + (double)rx);
     double yo = cam.pixel_size * ((double)y + (double)ry);
     const double a = cam.half_width - xo, b = cam.half_height - yo;
     const double* m = cam.inv;
-    d4 pixel = mk(((m[0] * a + m[1] * b) + cc.nm2[0]) + cc.m3[0], ((m[4] * a + m[5] * b) + cc.nm2[1]) + cc.m3[1],
-                  ((m[8] * a + m[9] * b) + cc.nm2[2]) + cc.m3[2],
-                  A ? 1.0 : ((m[12] * a + m[13] * b) + cc.nm2[3]) + cc.m3[3]);
-    d4 origin = cc.origin;
+    d4 pixel = mk(((m[0] * a + m[1] * b) + (-m[2])) + m[3], ((m[4] * a + m[5] * b) + (-m[6])) + m[7],
+                  ((m[8] * a + m[9] * b) + (-m[10])) + m[11],
+                  A ? 1.0 : ((m[12] * a + m[13] * b) + (-m[14])) + m[15]);
+    d4 origin = ld4(cam.origin);
     if (A) origin.w = 1.0;
     d4 dir = (PTMI_ABLATE & 2) ? sub4(pixel, origin) : normv<A>(sub4(pixel, origin));
     if (kDof && cam.aperture != 0) {
@@ -1153,7 +1139,6 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
     const float fgi = (float)(seed / (double)S.n_list);
     const float fgi2 = (float)(seed / (double)samples);
     double cr = 0.0, cg = 0.0, cb = 0.0;
-    const CamConst cc = cam_const(S.cam);
     // Camera rays are produced in wave-wide batches into a kCamDepth-deep per-lane
     // ring buffer (LDS) and consumed by path regeneration: generating them at the
     // moment each lane needs one would run the camera block (2 noise3D + the
@@ -1186,7 +1171,7 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
         if (n_need >= kRefillNeed || n_starve >= kRefillStarve || (n_starve > 0 && !__any(active))) {
             if (need) {
                 d4 ro, rd;
-                ray_for_pixel<(FL & F_DOF) != 0, A>(S.cam, cc, sunf, (unsigned)px, (unsigned)py,
+                ray_for_pixel<(FL & F_DOF) != 0, A>(S.cam, sunf, (unsigned)px, (unsigned)py,
                                                     noise3d(fgi, (float)n_gen, fgi2), noise3d(fgi, fgi2, (float)n_gen),
                                                     (int)n_gen, ro, rd);
                 int slot = hb + nb;
