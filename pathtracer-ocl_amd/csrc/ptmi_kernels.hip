@@ -27,11 +27,21 @@
 #define PTMI_STATS 0
 #endif
 #if PTMI_STATS
-__device__ unsigned long long ptmi_stats[12];  // [11]: eager re-walks  // walks, node4, leaves, tri tests, verifies, gate rejects, obj gate
+__device__ unsigned long long ptmi_stats[20];  // [11]: eager re-walks  // walks, node4, leaves, tri tests, verifies, gate rejects, obj gate
                                                // pass, group obj tests, walk phases, lanes in phases, loop iters
 #define PTMI_COUNT(i) atomicAdd(&ptmi_stats[i], 1ull)
+// [12..16]: per-wave shader-clock cycles in refill / closest-prims+gate / walk phases /
+// shade / whole loop (lane 0 of each wave; wave lifetime, other waves' issue included)
+#define PTMI_TSTAMP(v) const unsigned long long v = clock64()
+#define PTMI_TADD(i, t0) \
+    do { \
+        const unsigned long long t1_ = clock64(); \
+        if ((threadIdx.x & 63) == 0) atomicAdd(&ptmi_stats[i], t1_ - (t0)); \
+    } while (0)
 #else
 #define PTMI_COUNT(i) ((void)0)
+#define PTMI_TSTAMP(v) ((void)0)
+#define PTMI_TADD(i, t0) ((void)0)
 #endif
 
 namespace ptmi {
@@ -206,9 +216,11 @@ __device__ __forceinline__ float noise3d(float x, float y, float z) {
     float c = z * 237.212f;
     float s = (a + b) + c;
     if (PTMI_ABLATE & 32) s = s * 1e-6f;  // DIAGNOSTIC: small-argument sin path only
+    // Every call site passes finite floats below 2^33 (fgi, fgi2 in [0, 1], sample and
+    // bounce indices and n*n as u32), so s, sin(s) and v are finite and ocml fract's
+    // NaN / inf cases (fract(NaN) = NaN, fract(inf) = 0) are unreachable.
     float v = sinf(s) * 43758.5453f;
-    float r = fminf(v - floorf(v), 0x1.fffffep-1f);
-    return isnan(v) ? v : (isinf(v) ? 0.0f : r);
+    return fminf(v - floorf(v), 0x1.fffffep-1f);
 }
 
 // checkAxis (tracer.cl:250-268)
@@ -250,8 +262,9 @@ struct Hit {
 // list order, so a tie in t is broken by the object's list index: the winner is
 // the lexicographic minimum (t, key) -- the same candidate.  Candidates of one
 // object are still produced in the reference's order (strict < keeps the first).
+// Evaluated without short-circuits: compares and mask ops, no exec-mask branches.
 __device__ __forceinline__ bool better(const Hit& h, double t, int key) {
-    return t > kEps && (t < h.t || (t == h.t && key < h.key));
+    return (t > kEps) & ((t < h.t) | ((t == h.t) & (key < h.key)));
 }
 // Triangles of one group object are recorded by the reference in increasing
 // triangle index (nodes are numbered, and their triangles appended, in the same
@@ -558,25 +571,43 @@ template <int FL>
 __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 rd) {
     constexpr bool A = !(FL & F_PROJ);
     Hit h{1024.0, -1, -1, -1, -1, 0.0, 0.0};
-    for (int p = 0; p < ((PTMI_ABLATE & 8) ? 0 : S.n_planes); p++) {  // intersectPlane (478-483): row 1 only
-        const PlaneRec& P = S.planes[p];
-        const double oy = ((P.row1[0] * ro.x + P.row1[1] * ro.y) + P.row1[2] * ro.z) + (A ? P.row1[3] : P.row1[3] * ro.w);
-        const double dy0 = (P.row1[0] * rd.x + P.row1[1] * rd.y) + P.row1[2] * rd.z;
-        const double dy = A ? dy0 : dy0 + P.row1[3] * rd.w;
-        const double q = (PTMI_ABLATE & 64) ? -oy * __builtin_amdgcn_rcp(dy) : -oy / dy;  // DIAGNOSTIC 64
-        consider_sel(h, fabs(dy) > kEps ? q : 0.0, P.slot, P.key);
-    }
-    for (int q = 0; q < ((PTMI_ABLATE & 16) ? 0 : S.n_spheres_st); q++) {  // scale+translate spheres
-        const SphereRec& Q = S.spheres[q];
-        d4 o, d;
-        if constexpr (A) {
-            o = mk(Q.m0 * ro.x + Q.m3, Q.m5 * ro.y + Q.m7, Q.m10 * ro.z + Q.m11, 1.0);
-            d = mk(Q.m0 * rd.x, Q.m5 * rd.y, Q.m10 * rd.z, 0.0);
-        } else {
-            o = mk(Q.m0 * ro.x + Q.m3 * ro.w, Q.m5 * ro.y + Q.m7 * ro.w, Q.m10 * ro.z + Q.m11 * ro.w, Q.m15 * ro.w);
-            d = mk(Q.m0 * rd.x + Q.m3 * rd.w, Q.m5 * rd.y + Q.m7 * rd.w, Q.m10 * rd.z + Q.m11 * rd.w, Q.m15 * rd.w);
+    // Plane and sphere records are scalar loads; the next object's record is loaded
+    // while the current one is intersected (its latency is otherwise exposed on
+    // every object).  Duplicate-free: the last iteration re-loads its own record.
+    // Planes come first, in increasing list index, so inside the plane loop a tie in
+    // t can never favour the later plane: strict t < h.t is better() there.
+    const int np = (PTMI_ABLATE & 8) ? 0 : S.n_planes;
+    if (np > 0) {
+        PlaneRec P = S.planes[0];
+        for (int p = 0; p < np; p++) {  // intersectPlane (478-483): row 1 only
+            const PlaneRec Pn = S.planes[p + 1 < np ? p + 1 : p];
+            const double oy = ((P.row1[0] * ro.x + P.row1[1] * ro.y) + P.row1[2] * ro.z) + (A ? P.row1[3] : P.row1[3] * ro.w);
+            const double dy0 = (P.row1[0] * rd.x + P.row1[1] * rd.y) + P.row1[2] * rd.z;
+            const double dy = A ? dy0 : dy0 + P.row1[3] * rd.w;
+            const double q = (PTMI_ABLATE & 64) ? -oy * __builtin_amdgcn_rcp(dy) : -oy / dy;  // DIAGNOSTIC 64
+            const bool c = (fabs(dy) > kEps) & (q > kEps) & (q < h.t);
+            h.t = c ? q : h.t;
+            h.obj = c ? P.slot : h.obj;
+            h.key = c ? P.key : h.key;
+            P = Pn;
         }
-        sphere_test<A>(h, o, d, Q.slot, Q.key);
+    }
+    const int nq = (PTMI_ABLATE & 16) ? 0 : S.n_spheres_st;
+    if (nq > 0) {
+        SphereRec Q = S.spheres[0];
+        for (int q = 0; q < nq; q++) {  // scale+translate spheres
+            const SphereRec Qn = S.spheres[q + 1 < nq ? q + 1 : q];
+            d4 o, d;
+            if constexpr (A) {
+                o = mk(Q.m0 * ro.x + Q.m3, Q.m5 * ro.y + Q.m7, Q.m10 * ro.z + Q.m11, 1.0);
+                d = mk(Q.m0 * rd.x, Q.m5 * rd.y, Q.m10 * rd.z, 0.0);
+            } else {
+                o = mk(Q.m0 * ro.x + Q.m3 * ro.w, Q.m5 * ro.y + Q.m7 * ro.w, Q.m10 * ro.z + Q.m11 * ro.w, Q.m15 * ro.w);
+                d = mk(Q.m0 * rd.x + Q.m3 * rd.w, Q.m5 * rd.y + Q.m7 * rd.w, Q.m10 * rd.z + Q.m11 * rd.w, Q.m15 * rd.w);
+            }
+            sphere_test<A>(h, o, d, Q.slot, Q.key);
+            Q = Qn;
+        }
     }
     int j = S.run_end[0];
     for (; j < S.run_end[1]; j++) {  // spheres with other matrices
@@ -1162,8 +1193,10 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
     bool active = false, pending = false;
     PathState P;
     Hit hp;
+    PTMI_TSTAMP(t_loop);
     for (;;) {
         if (!__any(active || nb > 0 || n_gen < c1)) break;
+        PTMI_TSTAMP(t_a);
         const bool need = nb < kCamDepth && n_gen < c1;
         const int n_need = __popcll(__ballot(need));
         const int n_starve = __popcll(__ballot(nb == 0 && !active && n_gen < c1));
@@ -1201,6 +1234,8 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
             nb--;
             active = true;
         }
+        PTMI_TADD(12, t_a);
+        PTMI_TSTAMP(t_b);
         // Closest hit.  Scenes with BVH groups defer the walks: a lane whose ray
         // needs one parks (pending, keeping its primitives' best in hp) and the
         // wave walks all parked lanes together once kWalkBatch are parked or no
@@ -1212,7 +1247,7 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
         bool ready = false;
         Hit h;
 #if PTMI_STATS
-        if ((FL & F_GROUPS) && (threadIdx.x & 63) == 0) atomicAdd(&ptmi_stats[10], 1ull);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&ptmi_stats[10], 1ull);
 #endif
         if (active && !pending) {
             if (P.dead) {
@@ -1228,6 +1263,8 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
                 }
             }
         }
+        PTMI_TADD(13, t_b);
+        PTMI_TSTAMP(t_c);
         if (FL & F_GROUPS) {
             const int n_pend = __popcll(__ballot(pending));
             if (n_pend >= kWalkBatch || (n_pend > 0 && !__any(ready))) {
@@ -1245,13 +1282,17 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
                 }
             }
         }
+        PTMI_TADD(14, t_c);
+        PTMI_TSTAMP(t_d);
         if (ready && bounce_shade<FL>(S, P, h, fgi, n_cur)) {
             cr = cr + P.ar;  // colors += accumColor (tracer.cl:1179)
             cg = cg + P.ag;
             cb = cb + P.ab;
             active = false;
         }
+        PTMI_TADD(15, t_d);
     }
+    PTMI_TADD(16, t_loop);
     double* o = out + ((size_t)blockIdx.y * ((size_t)W * H) + i) * 4;
     o[0] = cr;
     o[1] = cg;
@@ -1405,9 +1446,9 @@ hipError_t launch_seeds(double* seeds, uint32_t n, uint64_t stream, hipStream_t 
 #if PTMI_STATS
 namespace ptmi {
 int stats_read(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi_stats), sizeof(unsigned long long) * 12) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi_stats), sizeof(unsigned long long) * 20) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[12] = {0};
+        unsigned long long z[20] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(ptmi_stats), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

@@ -18,13 +18,14 @@ if scene.startswith("adv:"):
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 W, H = 1280, 960
 lib = api.load_library()
-buf = (ctypes.c_ulonglong * 12)()
+buf = (ctypes.c_ulonglong * 20)()
 lib.ptmi_stats_read(buf, 1)
 objs, tris, grps, cam = scene_inputs(scene, W, H)
 api.Trace(objs, tris, grps, 0, spp, cam, seeds=layout.seeds_go_float64(W * H, 3))
 lib.ptmi_stats_read(buf, 1)
 names = ["walks", "node4", "leaves", "tri_tests", "verifies", "gate_rejects", "obj_gate_pass", "group_obj_tests",
-         "walk_phases", "lanes_in_phases", "wave_iterations", "eager_rewalks"]
+         "walk_phases", "lanes_in_phases", "wave_iterations", "eager_rewalks",
+         "cyc_refill", "cyc_prims_gate", "cyc_walk_phases", "cyc_shade", "cyc_loop"]
 v = dict(zip(names, buf))
 n = W * H * spp
 print(scene, "spp", spp)
@@ -32,3 +33,8 @@ print("  lanes per walk phase %.1f, wave iterations per walk phase %.1f" % (
     v["lanes_in_phases"] / max(v["walk_phases"], 1), v["wave_iterations"] / max(v["walk_phases"], 1)))
 for k in names:
     print("  %-16s %14d  per sample %8.3f  per walk %8.3f" % (k, v[k], v[k] / n, v[k] / max(v["walks"], 1)))
+tot = max(v["cyc_loop"], 1)
+for k in ("cyc_refill", "cyc_prims_gate", "cyc_walk_phases", "cyc_shade"):
+    print("  share %-16s %.3f" % (k, v[k] / tot))
+print("  cycles per walk phase %.0f, per wave iteration %.0f" % (
+    v["cyc_walk_phases"] / max(v["walk_phases"], 1), v["cyc_loop"] / max(v["wave_iterations"], 1)))
