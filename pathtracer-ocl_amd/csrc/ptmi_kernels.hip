@@ -543,14 +543,17 @@ __device__ __forceinline__ void consider_sel(Hit& h, double t, int obj, int key)
     h.tri = c ? -1 : h.tri;
 }
 
-// intersectSphere (tracer.cl:448-476) on an object-space ray.
+// intersectSphere (tracer.cl:448-476) on an object-space ray: the quadratic ...
 template <bool A>
-__device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int key) {
+__device__ __forceinline__ void sphere_quad(d4 o, d4 d, double& a, double& b, double& disc) {
     d4 vtc = mk(o.x - 0.0, o.y - 0.0, o.z - 0.0, A ? 0.0 : o.w - 1.0);
-    double a = dotv<A>(d, d);
-    double b = 2.0 * dotv<A>(d, vtc);
+    a = dotv<A>(d, d);
+    b = 2.0 * dotv<A>(d, vtc);
     double c = dotv<A>(vtc, vtc) - 1.0;
-    double disc = (b * b) - 4 * a * c;
+    disc = (b * b) - 4 * a * c;
+}
+// ... and its roots.
+__device__ __forceinline__ void sphere_roots(Hit& h, double a, double b, double disc, int slot, int key) {
     if (disc > 0.0) {
         // a > 0 and sq >= 0 give t1 <= t2 after rounding (rounding is monotonic),
         // so t2 can only be recorded as the winner when t1 itself is not a
@@ -563,6 +566,12 @@ __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int ke
             consider_sel(h, t2, slot, key);
         }
     }
+}
+template <bool A>
+__device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int key) {
+    double a, b, disc;
+    sphere_quad<A>(o, d, a, b, disc);
+    sphere_roots(h, a, b, disc, slot, key);
 }
 
 // findClosestIntersection (tracer.cl:537-742), one loop per object type.  Loop
@@ -577,37 +586,65 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     // Planes come first, in increasing list index, so inside the plane loop a tie in
     // t can never favour the later plane: strict t < h.t is better() there.
     const int np = (PTMI_ABLATE & 8) ? 0 : S.n_planes;
-    if (np > 0) {
-        PlaneRec P = S.planes[0];
-        for (int p = 0; p < np; p++) {  // intersectPlane (478-483): row 1 only
-            const PlaneRec Pn = S.planes[p + 1 < np ? p + 1 : p];
-            const double oy = ((P.row1[0] * ro.x + P.row1[1] * ro.y) + P.row1[2] * ro.z) + (A ? P.row1[3] : P.row1[3] * ro.w);
-            const double dy0 = (P.row1[0] * rd.x + P.row1[1] * rd.y) + P.row1[2] * rd.z;
-            const double dy = A ? dy0 : dy0 + P.row1[3] * rd.w;
-            const double q = (PTMI_ABLATE & 64) ? -oy * __builtin_amdgcn_rcp(dy) : -oy / dy;  // DIAGNOSTIC 64
-            const bool c = (fabs(dy) > kEps) & (q > kEps) & (q < h.t);
-            h.t = c ? q : h.t;
-            h.obj = c ? P.slot : h.obj;
-            h.key = c ? P.key : h.key;
-            P = Pn;
-        }
+    // intersectPlane (478-483): row 1 only.  Planes are taken two at a time so the
+    // two independent division chains overlap (then one odd plane).
+    auto plane_t = [&](const PlaneRec& P, double& q, bool& ok) {
+        const double oy = ((P.row1[0] * ro.x + P.row1[1] * ro.y) + P.row1[2] * ro.z) + (A ? P.row1[3] : P.row1[3] * ro.w);
+        const double dy0 = (P.row1[0] * rd.x + P.row1[1] * rd.y) + P.row1[2] * rd.z;
+        const double dy = A ? dy0 : dy0 + P.row1[3] * rd.w;
+        q = (PTMI_ABLATE & 64) ? -oy * __builtin_amdgcn_rcp(dy) : -oy / dy;  // DIAGNOSTIC 64
+        ok = (fabs(dy) > kEps) & (q > kEps);
+    };
+    auto plane_take = [&](const PlaneRec& P, double q, bool ok) {
+        const bool c = ok & (q < h.t);
+        h.t = c ? q : h.t;
+        h.obj = c ? P.slot : h.obj;
+        h.key = c ? P.key : h.key;
+    };
+    int p = 0;
+    for (; p + 1 < np; p += 2) {
+        const PlaneRec P0 = S.planes[p], P1 = S.planes[p + 1];
+        double q0, q1;
+        bool k0, k1;
+        plane_t(P0, q0, k0);
+        plane_t(P1, q1, k1);
+        plane_take(P0, q0, k0);
+        plane_take(P1, q1, k1);
+    }
+    if (p < np) {
+        const PlaneRec P0 = S.planes[p];
+        double q0;
+        bool k0;
+        plane_t(P0, q0, k0);
+        plane_take(P0, q0, k0);
     }
     const int nq = (PTMI_ABLATE & 16) ? 0 : S.n_spheres_st;
-    if (nq > 0) {
-        SphereRec Q = S.spheres[0];
-        for (int q = 0; q < nq; q++) {  // scale+translate spheres
-            const SphereRec Qn = S.spheres[q + 1 < nq ? q + 1 : q];
-            d4 o, d;
-            if constexpr (A) {
-                o = mk(Q.m0 * ro.x + Q.m3, Q.m5 * ro.y + Q.m7, Q.m10 * ro.z + Q.m11, 1.0);
-                d = mk(Q.m0 * rd.x, Q.m5 * rd.y, Q.m10 * rd.z, 0.0);
-            } else {
-                o = mk(Q.m0 * ro.x + Q.m3 * ro.w, Q.m5 * ro.y + Q.m7 * ro.w, Q.m10 * ro.z + Q.m11 * ro.w, Q.m15 * ro.w);
-                d = mk(Q.m0 * rd.x + Q.m3 * rd.w, Q.m5 * rd.y + Q.m7 * rd.w, Q.m10 * rd.z + Q.m11 * rd.w, Q.m15 * rd.w);
-            }
-            sphere_test<A>(h, o, d, Q.slot, Q.key);
-            Q = Qn;
+    auto sphere_ray = [&](const SphereRec& Q, d4& o, d4& d) {
+        if constexpr (A) {
+            o = mk(Q.m0 * ro.x + Q.m3, Q.m5 * ro.y + Q.m7, Q.m10 * ro.z + Q.m11, 1.0);
+            d = mk(Q.m0 * rd.x, Q.m5 * rd.y, Q.m10 * rd.z, 0.0);
+        } else {
+            o = mk(Q.m0 * ro.x + Q.m3 * ro.w, Q.m5 * ro.y + Q.m7 * ro.w, Q.m10 * ro.z + Q.m11 * ro.w, Q.m15 * ro.w);
+            d = mk(Q.m0 * rd.x + Q.m3 * rd.w, Q.m5 * rd.y + Q.m7 * rd.w, Q.m10 * rd.z + Q.m11 * rd.w, Q.m15 * rd.w);
         }
+    };
+    int q = 0;
+    for (; q + 1 < nq; q += 2) {  // two spheres at a time: overlapping quadratic setups
+        const SphereRec Q0 = S.spheres[q], Q1 = S.spheres[q + 1];
+        d4 o0, d0, o1, d1;
+        sphere_ray(Q0, o0, d0);
+        sphere_ray(Q1, o1, d1);
+        double a0, b0, disc0, a1, b1, disc1;
+        sphere_quad<A>(o0, d0, a0, b0, disc0);
+        sphere_quad<A>(o1, d1, a1, b1, disc1);
+        sphere_roots(h, a0, b0, disc0, Q0.slot, Q0.key);
+        sphere_roots(h, a1, b1, disc1, Q1.slot, Q1.key);
+    }
+    if (q < nq) {
+        const SphereRec Q0 = S.spheres[q];
+        d4 o0, d0;
+        sphere_ray(Q0, o0, d0);
+        sphere_test<A>(h, o0, d0, Q0.slot, Q0.key);
     }
     int j = S.run_end[0];
     for (; j < S.run_end[1]; j++) {  // spheres with other matrices
