@@ -236,7 +236,7 @@ int convert_scene(const uint8_t* objects, uint32_t n_obj, const uint8_t* tris, u
         if (o.type != 4) continue;
         RootRec rec;
         const int rc = build_object_index(tris, nodes, tri_off, tri_cnt, roots.data() + o.child_base, o.child_count,
-                                          index, &rec, err, err_len);
+                                          o.bb_min, o.bb_max, index, &rec, err, err_len);
         if (rc) return rc;
         o.child_base = (int32_t)root_rec.size();
         o.child_count = 1;

@@ -188,8 +188,8 @@ int32_t leaf_code(int32_t first, int32_t count) { return -((first << 3) | count)
 }  // namespace
 
 int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, const std::vector<int32_t>& tri_off,
-                       const std::vector<int32_t>& tri_cnt, const int32_t* roots, int n_roots, RootIndex& out,
-                       RootRec* rec, char* err, size_t err_len) {
+                       const std::vector<int32_t>& tri_cnt, const int32_t* roots, int n_roots, const double* gate_mn,
+                       const double* gate_mx, RootIndex& out, RootRec* rec, char* err, size_t err_len) {
     *rec = RootRec{};
     int32_t* entry = &rec->entry;
     const int32_t root = n_roots > 0 ? roots[0] : -1;  // for messages
@@ -203,18 +203,33 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
     while (!todo.empty()) {
         auto [g, path] = todo.back();
         todo.pop_back();
-        if (path.size() > 31) {
-            std::snprintf(err, err_len, "reference BVH deeper than 30 levels below root %d", root);
+        if (path.size() > 30) {
+            std::snprintf(err, err_len, "reference BVH deeper than 29 levels below root %d", root);
             return PTMI_ERR_UNSUPPORTED;
         }
+        // The chain: the group object's own gate box (tracer.cl:609), then the
+        // boxes of the reference nodes from the root down to this node (617-719).
         const int32_t off = (int32_t)out.chain_boxes.size();
-        for (int32_t k : path) {
+        ChainBox core;  // the intersection of the chain's boxes, stored after them
+        for (int k = 0; k < 3; k++) core.mn[k] = -HUGE_VAL, core.mx[k] = HUGE_VAL;
+        for (size_t i = 0; i <= path.size(); i++) {
             ChainBox b;
-            std::memcpy(b.mn, nodes[k].bb_min, 24);
-            std::memcpy(b.mx, nodes[k].bb_max, 24);
+            if (i == 0) {
+                std::memcpy(b.mn, gate_mn, 24);
+                std::memcpy(b.mx, gate_mx, 24);
+            } else {
+                std::memcpy(b.mn, nodes[path[i - 1]].bb_min, 24);
+                std::memcpy(b.mx, nodes[path[i - 1]].bb_max, 24);
+            }
             out.chain_boxes.push_back(b);
+            for (int a = 0; a < 3; a++) {
+                core.mn[a] = std::max(core.mn[a], b.mn[a]);  // NaN bounds leave the core unbounded
+                core.mx[a] = std::min(core.mx[a], b.mx[a]);  // there: no certificate is issued (NaN test)
+                if (b.mn[a] != b.mn[a] || b.mx[a] != b.mx[a]) core.mn[a] = core.mx[a] = NAN;
+            }
         }
-        const int32_t chain = (off << 5) | (int32_t)path.size();
+        out.chain_boxes.push_back(core);
+        const int32_t chain = (off << 5) | (int32_t)(path.size() + 1);
         for (int32_t t = tri_off[g]; t < tri_off[g] + tri_cnt[g]; t++) {
             const uint8_t* b = tris + (size_t)PTMI_TRIANGLE_BYTES * t;
             Prim p;

@@ -18,9 +18,10 @@ struct RootIndex {  // appended to by every root built into one scene
 // Build the traversal index of all triangles below the reference roots
 // roots[0..n_roots) of one group object (their subtrees in `nodes`, triangle
 // ranges tri_off/tri_cnt) into `out`; *rec receives the entry code and the
-// widened hull.  Returns PTMI_OK or an error.
+// widened hull.  Each triangle's gate chain starts with the object's own box
+// gate_mn/gate_mx (group space).  Returns PTMI_OK or an error.
 int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, const std::vector<int32_t>& tri_off,
-                       const std::vector<int32_t>& tri_cnt, const int32_t* roots, int n_roots, RootIndex& out,
-                       RootRec* rec, char* err, size_t err_len);
+                       const std::vector<int32_t>& tri_cnt, const int32_t* roots, int n_roots, const double* gate_mn,
+                       const double* gate_mx, RootIndex& out, RootRec* rec, char* err, size_t err_len);
 
 }  // namespace ptmi

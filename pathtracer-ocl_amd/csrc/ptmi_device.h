@@ -62,7 +62,9 @@ static_assert(sizeof(DevNode) == 64, "DevNode must stay 64 B");
 
 // Triangle in traversal-index leaf order; `n` is its index in the reference's
 // triangle list (tie-break order and DevTriShade slot), `chain` locates its gate
-// chain: ChainBox[chain >> 5 .. + (chain & 31)) (see ptmi_bvh.cpp).
+// chain: ChainBox[chain >> 5 .. + (chain & 31)), followed by the chain's core box
+// (the intersection of its boxes) at ChainBox[(chain >> 5) + (chain & 31)]
+// (see ptmi_bvh.cpp and chain_certified).
 struct alignas(16) DevTri {
     double p1[3];
     double e1[3];

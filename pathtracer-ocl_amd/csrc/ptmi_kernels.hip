@@ -314,6 +314,17 @@ __device__ __forceinline__ bool ray_box_t(d4 o, d4 d, const double* mn, const do
 // reference's det >= 1e-4); 1e-9 (1 + t) is orders of magnitude larger.
 __device__ __forceinline__ double prune_margin(double t) { return 1e-9 * (1.0 + fabs(t)); }
 
+// 1/d for the conservative (margin-widened) traversal tests only -- never for a
+// value the reference computes: v_rcp_f64 plus one Newton step (relative error
+// <= ~2^-40 from the hardware estimate's ~2^-23; every consumer widens by >= 2^-30);
+// zero / denormal / non-finite d takes the exact quotient.
+__device__ __forceinline__ double rcp_walk(double d) {
+    const double r0 = __builtin_amdgcn_rcp(d);
+    double r = fma(r0, fma(-d, r0, 1.0), r0);
+    if (!isfinite(r) || !(fabs(d) > 0x1p-1000)) r = 1.0 / d;
+    return r;
+}
+
 // One slab of intersectRayWithBox evaluated with the ray's reciprocal instead of
 // the reference's division: |a*r - RN(a/d)| <= 3u|a/d| (u = 2^-53), bounded here
 // by e = 2^-50 |a*r| + tiny.  Axes with |d| < EPSILON are computed exactly as the
@@ -356,6 +367,7 @@ __device__ __forceinline__ bool ray_box_ref(d4 o, d4 d, d4 r, const double* mn, 
 // Moller-Trumbore (tracer.cl:640-675) on the 3 live components: the w terms of
 // the reference's dot() products multiply a cross() result whose w is exactly 0.
 __device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o, d4 d);
+__device__ __forceinline__ bool chain_certified(const DevScene& S, int chain, d4 o, d4 d, double t);
 
 template <bool kVerify>
 __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 o, d4 d, int slot, int key, Hit& h,
@@ -398,7 +410,7 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 
         // tests.  The fast mode takes it tentatively; group_walks verifies the
         // final winner.
         if (kVerify && c != vchain) {
-            if (!verify_chain(S, c, o, d)) {
+            if (!chain_certified(S, c, o, d, t) && !verify_chain(S, c, o, d)) {
                 PTMI_COUNT(5);  // (stats build: gate rejections)
                 return;
             }
@@ -427,12 +439,38 @@ __device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o,
     const d4 r = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z, 0.0);  // recomputed: rare, and keeps r out of the walk
     const ChainBox* B = S.chains + (chain >> 5);
     const int len = chain & 31;
-    PTMI_COUNT(4);
+    PTMI_COUNT(17);  // (stats build: exact chain verifications, i.e. certificate failures)
     for (int i = 0; i < len; i++) {
         double a, b;
         if (!ray_box_ref(o, d, r, B[i].mn, B[i].mx, a, b)) return false;
     }
     return true;
+}
+
+// Certificate for the reference's gate chain of a hit at parameter t: the point
+// o + t d lies strictly inside the chain's core box (the intersection of all its
+// boxes) by a margin above the rounding of both this test and the reference's slab
+// arithmetic, on every axis the reference divides by (|d| >= EPSILON); on the
+// axes it treats as parallel (+-HUGE_VAL slabs) the origin itself lies strictly
+// inside.  Then every box's computed slab interval contains t, so
+// intersectRayWithBox passes for each of them (tmin <= t... < ...tmax) and
+// verify_chain would return true.  Margin per axis: 2^-46 (|t d| + |o| + |mn| + |mx|),
+// about 100x the 5 ulps the argument needs (error of o + t*d, plus the division's
+// 2 roundings relative to |mn - o|).  NaN anywhere fails every test: no certificate.
+__device__ __forceinline__ bool chain_certified(const DevScene& S, int chain, d4 o, d4 d, double t) {
+    const ChainBox& C = S.chains[(chain >> 5) + (chain & 31)];
+    const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+    bool ok = true;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const double td = t * dd[a];
+        const double p = oo[a] + td;
+        const double m = 0x1p-46 * (((fabs(td) + fabs(oo[a])) + fabs(C.mn[a])) + fabs(C.mx[a])) + 0x1p-1000;
+        const bool in_div = (p > C.mn[a] + m) & (p < C.mx[a] - m);
+        const bool in_par = (oo[a] > C.mn[a]) & (oo[a] < C.mx[a]);
+        ok = ok & (fabs(dd[a]) >= kEps ? in_div : in_par);
+    }
+    return ok;
 }
 
 // Conservative slab test against a widened traversal box: false only when no
@@ -454,19 +492,20 @@ __device__ __forceinline__ bool cull_box(d4 o, d4 r, double mnx, double mny, dou
 // can produce a winning t is reached); ties resolve through better_tri.
 template <bool kVerify>
 __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes,
-                                           const RootRec& R, int slot, int key, d4 o, d4 d, Hit& h, int& vchain) {
+                                           const RootRec& R, int slot, int key, d4 o, d4 d, d4 rw, Hit& h,
+                                           int& vchain) {
     // FP32 slab tests.  With of = (float)o, rf = (float)(1/d) (|rf| clamped to
     // 1e30) and t' = fma(b, rf, -RN(of*rf)), the computed slab bound differs from
     // the exact (b - o)/d by at most 2^-23 |r| (|b| + 2|o|) (FP32 roundings of o,
     // r, the product and the fma); each axis interval is widened by 4x that, so
     // the test only rejects boxes the exact line misses.
     float of[3], rf[3], ofr[3], dt[3];
-    const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+    const double oo[3] = {o.x, o.y, o.z}, rr[3] = {rw.x, rw.y, rw.z};
     float omax = 0.0f;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
         of[a] = (float)oo[a];
-        const float r = (float)(1.0 / dd[a]);
+        const float r = (float)rr[a];  // rcp_walk: within 2^-40 of 1/d before the float rounding
         rf[a] = fminf(fmaxf(r, -1e30f), 1e30f);  // NaN stays NaN
         ofr[a] = of[a] * rf[a];
         omax = fmaxf(omax, fabsf(of[a]));
@@ -694,9 +733,11 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
 }
 
 // Groups (tracer.cl:598-720), split in two so a wave can defer the walks
-// (see trace_kernel): group_needs_walk is the cheap part -- the object's exact
-// gate and the roots' hull culls against the current best -- and group_walks
-// walks every root that survives, updating h.
+// (see trace_kernel): group_needs_walk is the cheap part -- the conservative cull
+// of each object's traversal hull against the current best -- and group_walks
+// walks every index that survives, updating h.  The reference's exact box gates
+// (the object's, tracer.cl:609, and its nodes', 617-719) are checked per winning
+// triangle on its gate chain (chain_certified / verify_chain).
 template <bool A>
 __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd, const Hit& h) {
 #if defined(PTMI_EXP) && (PTMI_EXP & 2)
@@ -706,9 +747,7 @@ __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd
         const DevObject& ob = S.objs[j];
         const d4 o = xpt<A>(ob.inv, ob.st, ro);
         const d4 d = xdir<A>(ob.inv, ob.st, rd);
-        const d4 r = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z, 0.0);
-        double tmin, tmax;
-        if (!ray_box_ref(o, d, r, ob.bb_min, ob.bb_max, tmin, tmax)) continue;
+        const d4 r = mk(rcp_walk(d.x), rcp_walk(d.y), rcp_walk(d.z), 0.0);
         for (int ci = 0; ci < ob.child_count; ci++) {
             const RootRec& R = S.root_rec[ob.child_base + ci];
             double tn;
@@ -725,7 +764,7 @@ __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd
 // inside the divergent walk loop).
 template <bool A, bool kVerify>
 __device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes, d4 ro,
-                                                 d4 rd, Hit& h) {
+                                                 d4 rd, Hit& h, bool& cert) {
 #if defined(PTMI_EXP) && (PTMI_EXP & 1)
     return;
 #endif
@@ -733,11 +772,11 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restr
         const DevObject& ob = S.objs[j];
         const d4 o = xpt<A>(ob.inv, ob.st, ro);
         const d4 d = xdir<A>(ob.inv, ob.st, rd);
-        const d4 r = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z, 0.0);
-        double tmin, tmax;
+        const d4 r = mk(rcp_walk(d.x), rcp_walk(d.y), rcp_walk(d.z), 0.0);
         PTMI_COUNT(7);
-        if (!ray_box_ref(o, d, r, ob.bb_min, ob.bb_max, tmin, tmax)) continue;  // the object's gate (609)
-        PTMI_COUNT(6);
+        // The object's own gate (tracer.cl:609) is the first box of every triangle's
+        // gate chain, so it is checked with the rest of the chain (chain_certified /
+        // verify_chain), not here.
         int vchain = -1;
         for (int ci = 0; ci < ob.child_count; ci++) {
             const RootRec& R = S.root_rec[ob.child_base + ci];
@@ -745,8 +784,11 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restr
             if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
                          R.hull_mx[2], h.t + prune_margin(h.t), tn))
                 continue;
-            walk_index<kVerify>(S, stk, lds_nodes, R, j, ob.key, o, d, h, vchain);
+            walk_index<kVerify>(S, stk, lds_nodes, R, j, ob.key, o, d, r, h, vchain);
         }
+        // Tentative walks: certify the gate chain of a winner from this object while
+        // its object-space ray is at hand (a later object that takes over re-certifies).
+        if (!kVerify && h.tri >= 0 && h.obj == j) cert = chain_certified(S, h.chain, o, d, h.t);
     }
 }
 
@@ -761,20 +803,21 @@ template <bool A>
 __device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes, d4 ro, d4 rd,
                                             Hit& h) {
     const Hit h0 = h;
-    group_walks_impl<A, false>(S, stk, lds_nodes, ro, rd, h);
-    if (h.tri >= 0) {  // the winner is a triangle (h0 holds primitives only)
-        PTMI_COUNT(4);
+    bool cert = false;
+    group_walks_impl<A, false>(S, stk, lds_nodes, ro, rd, h, cert);
+#if !(defined(PTMI_EXP) && (PTMI_EXP & 8))
+    if (h.tri >= 0) PTMI_COUNT(4);
+    if (h.tri >= 0 && !cert) {  // the winner is a triangle (h0 holds primitives only) without certificate
         const DevObject& ob = S.objs[h.obj];
         const d4 o = xpt<A>(ob.inv, ob.st, ro);
         const d4 d = xdir<A>(ob.inv, ob.st, rd);
-#if !(defined(PTMI_EXP) && (PTMI_EXP & 8))
         if (!verify_chain(S, h.chain, o, d)) {
             PTMI_COUNT(11);  // (stats build: eager re-walks)
             h = h0;
-            group_walks_impl<A, true>(S, stk, lds_nodes, ro, rd, h);
+            group_walks_impl<A, true>(S, stk, lds_nodes, ro, rd, h, cert);
         }
-#endif
     }
+#endif
 }
 
 // schlick (tracer.cl:485-505)

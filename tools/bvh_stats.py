@@ -25,7 +25,7 @@ api.Trace(objs, tris, grps, 0, spp, cam, seeds=layout.seeds_go_float64(W * H, 3)
 lib.ptmi_stats_read(buf, 1)
 names = ["walks", "node4", "leaves", "tri_tests", "verifies", "gate_rejects", "obj_gate_pass", "group_obj_tests",
          "walk_phases", "lanes_in_phases", "wave_iterations", "eager_rewalks",
-         "cyc_refill", "cyc_prims_gate", "cyc_walk_phases", "cyc_shade", "cyc_loop"]
+         "cyc_refill", "cyc_prims_gate", "cyc_walk_phases", "cyc_shade", "cyc_loop", "exact_chain_verifies"]
 v = dict(zip(names, buf))
 n = W * H * spp
 print(scene, "spp", spp)
