@@ -21,27 +21,47 @@
 #ifndef PTMI_ABLATE
 #define PTMI_ABLATE 0
 #endif
-// PTMI_STATS: DIAGNOSTIC counting build (make stats) -- tallies traversal events
-// into ptmi_stats[] (read with ptmi_stats_read); the product has PTMI_STATS == 0.
+// PTMI_STATS: DIAGNOSTIC builds -- 1 (make stats): tallies traversal events into
+// ptmi_stats[] (read with ptmi_stats_read); 2 (make timers): per-wave phase clocks
+// and per-wave counters only (the per-lane event atomics of 1 distort timing).
+// The product has PTMI_STATS == 0.
 #ifndef PTMI_STATS
 #define PTMI_STATS 0
 #endif
 #if PTMI_STATS
-__device__ unsigned long long ptmi_stats[20];  // [11]: eager re-walks  // walks, node4, leaves, tri tests, verifies, gate rejects, obj gate
-                                               // pass, group obj tests, walk phases, lanes in phases, loop iters
-#define PTMI_COUNT(i) atomicAdd(&ptmi_stats[i], 1ull)
-// [12..16]: per-wave shader-clock cycles in refill / closest-prims+gate / walk phases /
-// shade / whole loop (lane 0 of each wave; wave lifetime, other waves' issue included)
-#define PTMI_TSTAMP(v) const unsigned long long v = clock64()
-#define PTMI_TADD(i, t0) \
-    do { \
-        const unsigned long long t1_ = clock64(); \
-        if ((threadIdx.x & 63) == 0) atomicAdd(&ptmi_stats[i], t1_ - (t0)); \
+// Counters (tools/bvh_stats.py names them): [0] walks [1] node4 visits [2] leaves
+// [3] triangle tests [4] certified winners [5] gate rejections [6] (unused) [7] group
+// object tests [8] walk phases [9] lanes in phases [10] wave loop iterations [11] eager
+// re-walks [12..16] shader-clock cycles in refill / closest-prims+gate / walk phases /
+// shade / whole loop [17] exact chain verifications [18] cycles in walk loops
+// [19] wave-level walk loop iterations.
+__device__ unsigned long long ptmi_stats[24];
+// Per-wave accumulators (one writer per wave: the first active lane), flushed to
+// ptmi_stats with one atomic per counter when the wave leaves its loop, so clock
+// and per-wave counts do not serialise on global atomics.
+__shared__ unsigned long long ptmi_wstat[4][24];
+#define PTMI_FIRST_ACTIVE() ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1)
+#define PTMI_WADD(i, v)                                                \
+    do {                                                               \
+        const unsigned long long v_ = (v);                             \
+        if (PTMI_FIRST_ACTIVE()) ptmi_wstat[threadIdx.x >> 6][i] += v_; \
     } while (0)
+#if PTMI_STATS == 2
+#define PTMI_COUNT(i) ((void)0)
+#else
+#define PTMI_COUNT(i) atomicAdd(&ptmi_stats[i], 1ull)
+#endif
+#define PTMI_TSTAMP(v) const unsigned long long v = clock64()
+#define PTMI_TADD(i, t0) PTMI_WADD(i, clock64() - (t0))
+#define PTMI_TADD_ACTIVE(i, t0) PTMI_WADD(i, clock64() - (t0))
+#define PTMI_COUNT_ACTIVE(i) PTMI_WADD(i, 1ull)
 #else
 #define PTMI_COUNT(i) ((void)0)
 #define PTMI_TSTAMP(v) ((void)0)
 #define PTMI_TADD(i, t0) ((void)0)
+#define PTMI_TADD_ACTIVE(i, t0) ((void)0)
+#define PTMI_COUNT_ACTIVE(i) ((void)0)
+#define PTMI_WADD(i, v) ((void)0)
 #endif
 
 namespace ptmi {
@@ -517,20 +537,31 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
     int cur = R.entry;
     PTMI_COUNT(0);
     while (true) {
+        PTMI_COUNT_ACTIVE(19);  // (stats: wave-level walk loop iterations)
         if (cur >= 0) {
             PTMI_COUNT(1);
-            // the first kLdsNodes Node4s (the top levels, ptmi_bvh.cpp) are staged in LDS
-            const Node4& N = cur < kLdsNodes ? lds_nodes[cur] : S.nodes4[cur];
+            // The node's 112 B as seven 16-B loads issued together (one wait), from LDS
+            // for the first kLdsNodes Node4s (the top levels, ptmi_bvh.cpp), else global.
+            const float4* src = cur < kLdsNodes ? reinterpret_cast<const float4*>(lds_nodes) + 7 * cur
+                                                : reinterpret_cast<const float4*>(S.nodes4) + 7 * cur;
+            float4 q[7];
+#pragma unroll
+            for (int u = 0; u < 7; u++) q[u] = src[u];
+            const float mnx[4] = {q[0].x, q[0].y, q[0].z, q[0].w}, mny[4] = {q[1].x, q[1].y, q[1].z, q[1].w};
+            const float mnz[4] = {q[2].x, q[2].y, q[2].z, q[2].w}, mxx[4] = {q[3].x, q[3].y, q[3].z, q[3].w};
+            const float mxy[4] = {q[4].x, q[4].y, q[4].z, q[4].w}, mxz[4] = {q[5].x, q[5].y, q[5].z, q[5].w};
+            const int ch[4] = {__float_as_int(q[6].x), __float_as_int(q[6].y), __float_as_int(q[6].z),
+                               __float_as_int(q[6].w)};
             const double limd = h.t + prune_margin(h.t);
             const float lim = (float)limd * (1.0f + 0x1p-22f) + 0x1p-100f;  // >= limd
             float k[4];
             int c[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                c[i] = N.child[i];
-                const float ax = fmaf(N.mn[0][i], rf[0], -ofr[0]), bx = fmaf(N.mx[0][i], rf[0], -ofr[0]);
-                const float ay = fmaf(N.mn[1][i], rf[1], -ofr[1]), by = fmaf(N.mx[1][i], rf[1], -ofr[1]);
-                const float az = fmaf(N.mn[2][i], rf[2], -ofr[2]), bz = fmaf(N.mx[2][i], rf[2], -ofr[2]);
+                c[i] = ch[i];
+                const float ax = fmaf(mnx[i], rf[0], -ofr[0]), bx = fmaf(mxx[i], rf[0], -ofr[0]);
+                const float ay = fmaf(mny[i], rf[1], -ofr[1]), by = fmaf(mxy[i], rf[1], -ofr[1]);
+                const float az = fmaf(mnz[i], rf[2], -ofr[2]), bz = fmaf(mxz[i], rf[2], -ofr[2]);
                 const float tn = fmaxf(fmaxf(fminf(ax, bx) - dt[0], fminf(ay, by) - dt[1]), fminf(az, bz) - dt[2]);
                 const float tf = fminf(fminf(fmaxf(ax, bx) + dt[0], fmaxf(ay, by) + dt[1]), fmaxf(az, bz) + dt[2]);
                 // (NaN bounds -- a NaN ray -- fail every test: the child is entered.)
@@ -784,7 +815,9 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restr
             if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
                          R.hull_mx[2], h.t + prune_margin(h.t), tn))
                 continue;
+            PTMI_TSTAMP(t_w);
             walk_index<kVerify>(S, stk, lds_nodes, R, j, ob.key, o, d, r, h, vchain);
+            PTMI_TADD_ACTIVE(18, t_w);  // (stats: cycles in walk loops)
         }
         // Tentative walks: certify the gate chain of a winner from this object while
         // its object-space ray is at hand (a later object that takes over re-certifies).
@@ -1231,6 +1264,9 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
         for (int k = threadIdx.x; k < nl; k += 256) node_lds4[k] = src[k];
         __syncthreads();
     }
+#if PTMI_STATS
+    if ((threadIdx.x & 63) < 24) ptmi_wstat[threadIdx.x >> 6][threadIdx.x & 63] = 0;
+#endif
     const int W = S.cam.width, H = S.cam.height;
     const int tiles_x = (W + kTile - 1) / kTile;
     const int tiles_y = (H + kTile - 1) / kTile;
@@ -1327,7 +1363,7 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
         bool ready = false;
         Hit h;
 #if PTMI_STATS
-        if ((threadIdx.x & 63) == 0) atomicAdd(&ptmi_stats[10], 1ull);
+        PTMI_WADD(10, 1ull);
 #endif
         if (active && !pending) {
             if (P.dead) {
@@ -1348,12 +1384,8 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
         if (FL & F_GROUPS) {
             const int n_pend = __popcll(__ballot(pending));
             if (n_pend >= kWalkBatch || (n_pend > 0 && !__any(ready))) {
-#if PTMI_STATS
-                if ((threadIdx.x & 63) == 0) {
-                    atomicAdd(&ptmi_stats[8], 1ull);
-                    atomicAdd(&ptmi_stats[9], (unsigned long long)n_pend);
-                }
-#endif
+                PTMI_WADD(8, 1ull);
+                PTMI_WADD(9, (unsigned long long)n_pend);
                 if (pending) {
                     h = hp;
                     group_walks<A>(S, stk, node_lds, P.ro, P.rd, h);
@@ -1373,6 +1405,11 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
         PTMI_TADD(15, t_d);
     }
     PTMI_TADD(16, t_loop);
+#if PTMI_STATS
+    if (PTMI_FIRST_ACTIVE())
+        for (int k = 0; k < 24; k++)
+            if (ptmi_wstat[threadIdx.x >> 6][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[threadIdx.x >> 6][k]);
+#endif
     double* o = out + ((size_t)blockIdx.y * ((size_t)W * H) + i) * 4;
     o[0] = cr;
     o[1] = cg;
@@ -1526,9 +1563,9 @@ hipError_t launch_seeds(double* seeds, uint32_t n, uint64_t stream, hipStream_t 
 #if PTMI_STATS
 namespace ptmi {
 int stats_read(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi_stats), sizeof(unsigned long long) * 20) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi_stats), sizeof(unsigned long long) * 24) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[20] = {0};
+        unsigned long long z[24] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(ptmi_stats), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

@@ -18,14 +18,15 @@ if scene.startswith("adv:"):
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 W, H = 1280, 960
 lib = api.load_library()
-buf = (ctypes.c_ulonglong * 20)()
+buf = (ctypes.c_ulonglong * 24)()
 lib.ptmi_stats_read(buf, 1)
 objs, tris, grps, cam = scene_inputs(scene, W, H)
 api.Trace(objs, tris, grps, 0, spp, cam, seeds=layout.seeds_go_float64(W * H, 3))
 lib.ptmi_stats_read(buf, 1)
 names = ["walks", "node4", "leaves", "tri_tests", "verifies", "gate_rejects", "obj_gate_pass", "group_obj_tests",
          "walk_phases", "lanes_in_phases", "wave_iterations", "eager_rewalks",
-         "cyc_refill", "cyc_prims_gate", "cyc_walk_phases", "cyc_shade", "cyc_loop", "exact_chain_verifies"]
+         "cyc_refill", "cyc_prims_gate", "cyc_walk_phases", "cyc_shade", "cyc_loop", "exact_chain_verifies",
+         "cyc_walk_loops", "walk_loop_wave_iters"]
 v = dict(zip(names, buf))
 n = W * H * spp
 print(scene, "spp", spp)
@@ -38,3 +39,8 @@ for k in ("cyc_refill", "cyc_prims_gate", "cyc_walk_phases", "cyc_shade"):
     print("  share %-16s %.3f" % (k, v[k] / tot))
 print("  cycles per walk phase %.0f, per wave iteration %.0f" % (
     v["cyc_walk_phases"] / max(v["walk_phases"], 1), v["cyc_loop"] / max(v["wave_iterations"], 1)))
+print("  walk-loop cycles per phase %.0f, loop iterations per phase %.1f, cycles per loop iteration %.0f" % (
+    v["cyc_walk_loops"] / max(v["walk_phases"], 1), v["walk_loop_wave_iters"] / max(v["walk_phases"], 1),
+    v["cyc_walk_loops"] / max(v["walk_loop_wave_iters"], 1)))
+print("  camera/prims/shade cycles per non-walk wave iteration %.0f" % (
+    (v["cyc_refill"] + v["cyc_prims_gate"] + v["cyc_shade"]) / max(v["wave_iterations"], 1)))
