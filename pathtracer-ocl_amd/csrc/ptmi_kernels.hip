@@ -14,6 +14,7 @@
 #include <stdint.h>
 
 #include "ptmi_device.h"
+#include "ptmi_sinf.h"
 
 // PTMI_ABLATE: DIAGNOSTIC builds only (make ablate) -- removes a component to
 // measure its share of the run time.  Images from such builds are wrong by
@@ -239,7 +240,15 @@ __device__ __forceinline__ float noise3d(float x, float y, float z) {
     // Every call site passes finite floats below 2^33 (fgi, fgi2 in [0, 1], sample and
     // bounce indices and n*n as u32), so s, sin(s) and v are finite and ocml fract's
     // NaN / inf cases (fract(NaN) = NaN, fract(inf) = 0) are unreachable.
-    float v = sinf(s) * 43758.5453f;
+    // ocml's sin_f32, bit for bit; below 2^19 (every bench argument) with the
+    // specialised reduction of ptmi_sinf.h, above it through ocml itself.
+    float sn;
+    if (fabsf(s) < 0x1p19f) {
+        sn = sinf_lt19(s);
+    } else {
+        sn = sinf(s);
+    }
+    float v = sn * 43758.5453f;
     return fminf(v - floorf(v), 0x1.fffffep-1f);
 }
 

@@ -1,0 +1,126 @@
+// ptmi_sinf.h -- the reference RNG's float sin (noise3D, tracer.cl:314-317, whose
+// sin(float) is ROCm device-libs' __ocml_sin_f32) with the same result bits for
+// every finite |x| < 2^19 and a cheaper argument reduction for 2^17 <= |x| < 2^19.
+//
+// ocml reduces |x| >= 2^17 with a general Payne-Hanek step: seven chained 32x32->64
+// multiplies of the mantissa by 224 bits of 2/pi, then ~20 selects that pick a
+// 96-bit window of the product by the exponent, then the normalisation of that
+// window into a float hi/lo pair.  The noise arguments of the bench scenes lie
+// below 2^19 (sample index <= 2047: 237.212 n + ... < 5.3e5), where the exponent
+// is 144 or 145: the window is fixed (product words p4..p7, shift 152 - e) and
+// every select folds away.  The four least significant table words only reach
+// the window through the carry into p4, whose bits end ~90 places below the
+// binary point of x * 2/pi: leaving them out (3 multiplies instead of 7) changes no
+// result bit in the domain -- checked for every float |x| < 2^19 against the
+// oracle's restatement (tools/sinf_check.cpp) and against the device library
+// itself (tests/test_gpu_rng.py).  Without p4 as well, 38 floats would differ.
+// The small-argument path, the polynomials and the sign logic are ocml's,
+// operation for operation (cf. oracle/ocml_sinf.h, verified against ocml over
+// all 2^32 floats).
+//
+// Plain C++ on bit patterns (fshr / clz / fmaf), so the same source compiles for
+// gfx950 (v_alignbit_b32, v_ffbh_u32, v_fma_f32) and for a host-side check.
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#ifndef PTMI_SINF_FN
+#define PTMI_SINF_FN __device__ __forceinline__
+#endif
+
+namespace ptmi {
+
+PTMI_SINF_FN uint32_t sf_bits(float f) { return __builtin_bit_cast(uint32_t, f); }
+PTMI_SINF_FN float sf_float(uint32_t u) { return __builtin_bit_cast(float, u); }
+// llvm.fshr.i32 (s taken mod 32) -- one v_alignbit_b32 on the GPU -- and fshl for a
+// constant 0 < s < 32; clz with clz(0) = 32, as ocml uses them.
+PTMI_SINF_FN uint32_t sf_fshr(uint32_t a, uint32_t b, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(a, b, s);
+#else
+    return (uint32_t)((((uint64_t)a << 32) | b) >> (s & 31u));  // host build of tools/sinf_check.cpp
+#endif
+}
+PTMI_SINF_FN uint32_t sf_fshl(uint32_t a, uint32_t b, uint32_t s) { return sf_fshr(a, b, 32u - s); }
+PTMI_SINF_FN uint32_t sf_clz(uint32_t v) { return v ? (uint32_t)__builtin_clz(v) : 32u; }
+
+// __ocmlpriv_trigredsmall_f32 (ISA >= 9.0): 3-constant Cody-Waite, |x| < 2^17.
+PTMI_SINF_FN float sf_redux_small(float x, int& q) {
+    const float t = x * sf_float(0x3F22F983u);  // 2/pi
+    const float r = rintf(t);
+    float a = fmaf(r, sf_float(0xBFC90FDAu), x);
+    a = fmaf(r, sf_float(0xB3A22168u), a);
+    a = fmaf(r, sf_float(0xA7C234C4u), a);
+    q = ((int)r) & 3;
+    return a;
+}
+
+// __ocmlpriv_trigredlarge_f32 specialised to 2^17 <= x < 2^19 (exponent 144, 145).
+PTMI_SINF_FN float sf_redux_large_17_19(float x, int& q) {
+    const uint32_t bits = sf_bits(x);
+    const uint32_t e = bits >> 23;
+    const uint64_t m = (uint64_t)((bits & 0x7FFFFFu) | 0x800000u);
+    // mantissa * 2/pi words w4..w6: the carry of w0..w3 into p4 is dropped (see header)
+    uint64_t t = m * 4230436817ull;
+    const uint32_t p4 = (uint32_t)t;
+    t = (t >> 32) + m * 1313084713ull;
+    const uint32_t p5 = (uint32_t)t;
+    t = (t >> 32) + m * 2734261102ull;
+    const uint32_t p6 = (uint32_t)t;
+    const uint32_t p7 = (uint32_t)(t >> 32);
+    // ocml's window for e - 120 in [0, 31]: (p7, p6, p5, p4) shifted by 32 - (e - 120)
+    const uint32_t s61 = 152u - e;
+    const uint32_t a65 = sf_fshr(p7, p6, s61);
+    const uint32_t a66 = sf_fshr(p6, p5, s61);
+    const uint32_t a67 = sf_fshr(p5, p4, s61);
+    // from here on ocml's normalisation, unchanged
+    const uint32_t a68 = a65 >> 29;
+    const uint32_t a69 = sf_fshl(a65, a66, 2), a70 = sf_fshl(a66, a67, 2), a71 = sf_fshl(a67, p4, 2);
+    const uint32_t a72 = a68 & 1u;
+    const uint32_t a73 = 0u - a72;
+    const uint32_t a74 = a68 << 31;
+    const uint32_t a75 = a69 ^ a73, a76 = a70 ^ a73, a77 = a71 ^ a73;
+    const uint32_t a78 = sf_clz(a75);
+    const uint32_t a79 = 31u - a78;
+    const uint32_t a80 = sf_fshr(a75, a76, a79);
+    const uint32_t a81 = sf_fshr(a76, a77, a79);
+    const float hi = sf_float(((a80 >> 9) - (a78 << 23)) + 1056964608u + a74);
+    const uint32_t a88 = sf_fshl(a80, a81, 23);
+    const uint32_t a89 = sf_clz(a88);
+    const uint32_t a91 = sf_fshr(a88, a81, ~a89);
+    const float lo = sf_float(((a91 >> 9) - ((a89 + a78) << 23)) + 855638016u + a74);
+    const float pio2_hi = sf_float(0x3FC90FDAu), pio2_mid = sf_float(0x33A22168u);
+    const float p = hi * pio2_hi;
+    float e1 = fmaf(hi, pio2_hi, -p);
+    e1 = fmaf(hi, pio2_mid, e1);
+    e1 = fmaf(lo, pio2_hi, e1);
+    q = (int)((a72 + (a65 >> 30)) & 3u);
+    return e1 + p;
+}
+
+// __ocml_sin_f32 for finite |x| < 2^19 (callers route everything else to ocml).
+PTMI_SINF_FN float sinf_lt19(float x) {
+    const float ax = fabsf(x);
+    int q;
+    float r;
+    if (ax < 131072.0f) {
+        r = sf_redux_small(ax, q);
+    } else {
+        r = sf_redux_large_17_19(ax, q);
+    }
+    // __ocmlpriv_sincosred_f32 and the quadrant / sign fix-ups
+    const float x2 = r * r;
+    float s = fmaf(x2, sf_float(0xB94C1982u), sf_float(0x3C0881C4u));
+    s = fmaf(x2, s, sf_float(0xBE2AAA9Du));
+    s = x2 * s;
+    s = fmaf(r, s, r);
+    float c = fmaf(x2, sf_float(0x37D75334u), sf_float(0xBAB64F3Bu));
+    c = fmaf(x2, c, sf_float(0x3D2AABF7u));
+    c = fmaf(x2, c, sf_float(0xBF000004u));
+    c = fmaf(x2, c, 1.0f);
+    const uint32_t v = (q & 1) ? sf_bits(c) : sf_bits(s);
+    const uint32_t neg = (q > 1) ? 0x80000000u : 0u;
+    return sf_float((sf_bits(ax) ^ sf_bits(x)) ^ neg ^ v);
+}
+
+}  // namespace ptmi

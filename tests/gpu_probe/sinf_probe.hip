@@ -8,6 +8,7 @@
 
 #define PT_FN __host__ __device__ static inline
 #include "../../oracle/ocml_sinf.h"
+#include "../../pathtracer-ocl_amd/csrc/ptmi_sinf.h"  // the product's noise sin (kernel code)
 
 __global__ void sinf_check(uint64_t base, uint64_t count, unsigned long long* mism, unsigned int* first) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -27,6 +28,19 @@ __global__ void sinf_check(uint64_t base, uint64_t count, unsigned long long* mi
     }
 }
 
+// The kernel's sin for |x| < 2^19 (ptmi_sinf.h) against the device library.
+__global__ void ptmi_sinf_check(uint64_t base, uint64_t count, unsigned long long* mism, unsigned int* first) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t bits = (uint32_t)(base + i);
+    const float x = pto_bits2f(bits);
+    if (!(fabsf(x) < 0x1p19f)) return;
+    if (pto_f2bits(sinf(x)) != pto_f2bits(ptmi::sinf_lt19(x))) {
+        atomicAdd(mism, 1ull);
+        atomicMin(first, bits);
+    }
+}
+
 __global__ void sinf_eval(const float* in, float* out, uint64_t n) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = sinf(in[i]);
@@ -41,6 +55,25 @@ extern "C" int probe_sinf_all(unsigned long long* mismatches, unsigned int* firs
     const uint64_t chunk = 1ull << 28;
     for (uint64_t base = 0; base < (1ull << 32); base += chunk) {
         hipLaunchKernelGGL(sinf_check, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, chunk, dm, df);
+        if (hipGetLastError() != hipSuccess) return -2;
+    }
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    (void)hipMemcpy(mismatches, dm, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(first_bad, df, 4, hipMemcpyDeviceToHost);
+    (void)hipFree(dm);
+    (void)hipFree(df);
+    return 0;
+}
+
+extern "C" int probe_ptmi_sinf_all(unsigned long long* mismatches, unsigned int* first_bad) {
+    unsigned long long* dm;
+    unsigned int* df;
+    if (hipMalloc(&dm, 8) || hipMalloc(&df, 4)) return -1;
+    (void)hipMemset(dm, 0, 8);
+    (void)hipMemset(df, 0xff, 4);
+    const uint64_t chunk = 1ull << 28;
+    for (uint64_t base = 0; base < (1ull << 32); base += chunk) {
+        hipLaunchKernelGGL(ptmi_sinf_check, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, chunk, dm, df);
         if (hipGetLastError() != hipSuccess) return -2;
     }
     if (hipDeviceSynchronize() != hipSuccess) return -3;

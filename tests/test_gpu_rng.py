@@ -1,7 +1,7 @@
 """The reference RNG's float sin (tracer.cl:314-317 -> ocml __ocml_sin_f32):
-exhaustive bit-identity of the oracle's restatement (oracle/ocml_sinf.h) with
-the GPU device library over all 2^32 float inputs, and replay of ocml values
-on the host CPU (same code the CPU oracle runs)."""
+exhaustive bit-identity of the oracle's restatement (oracle/ocml_sinf.h) and of
+the kernel's own sin (csrc/ptmi_sinf.h) with the GPU device library, and replay
+of ocml values on the host CPU (same code the CPU oracle runs)."""
 import ctypes
 import os
 
@@ -20,6 +20,7 @@ def _lib():
     import torch  # noqa: F401  one HIP runtime per process (ptmi/_runtime.py)
     lib = ctypes.CDLL(LIB)
     lib.probe_sinf_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
+    lib.probe_ptmi_sinf_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
     lib.probe_sinf_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     return lib
 
@@ -28,6 +29,16 @@ def test_restated_sinf_bit_identical_all_floats():
     lib = _lib()
     m, f = ctypes.c_ulonglong(), ctypes.c_uint()
     assert lib.probe_sinf_all(ctypes.byref(m), ctypes.byref(f)) == 0
+    assert m.value == 0, "%d mismatches, first input bits 0x%08x" % (m.value, f.value)
+
+
+def test_kernel_sinf_bit_identical_below_2p19():
+    """The kernel's noise sin (pathtracer-ocl_amd/csrc/ptmi_sinf.h: ocml's sin_f32 with
+    the large-argument reduction specialised to 2^17 <= |x| < 2^19 and its four lowest
+    2/pi table words dropped) equals the device library for every float |x| < 2^19."""
+    lib = _lib()
+    m, f = ctypes.c_ulonglong(), ctypes.c_uint()
+    assert lib.probe_ptmi_sinf_all(ctypes.byref(m), ctypes.byref(f)) == 0
     assert m.value == 0, "%d mismatches, first input bits 0x%08x" % (m.value, f.value)
 
 
