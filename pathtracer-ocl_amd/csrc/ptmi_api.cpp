@@ -30,6 +30,7 @@ hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint3
 hipError_t launch_seeds(double* seeds, uint32_t n, uint64_t stream, hipStream_t st);
 hipError_t launch_plane_normals(DevObject* objs, int n, hipStream_t st);
 const void* trace_kernel_symbol(int flags);
+int trace_block_threads(int flags);
 }  // namespace ptmi
 
 using namespace ptmi;
@@ -437,10 +438,11 @@ int ptmi_scene_create_textured(int device_index, const void* objects, uint32_t n
     SCENE_TRY(hipGetDeviceProperties(&p, device_index));
     s->resident_waves = p.multiProcessorCount * 16;  // refined below from the occupancy query
     int blocks_per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, trace_kernel_symbol(s->flags), 256, 0) ==
+    const int block = trace_block_threads(s->flags);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, trace_kernel_symbol(s->flags), block, 0) ==
             hipSuccess &&
         blocks_per_cu > 0)
-        s->resident_waves = p.multiProcessorCount * blocks_per_cu * kWavesPerBlock;
+        s->resident_waves = p.multiProcessorCount * blocks_per_cu * (block / 64);
 #undef SCENE_TRY
     *out = s;
     return PTMI_OK;

@@ -152,6 +152,5 @@ struct DevScene {
 };
 
 constexpr int kTile = 8;          // a wave64 covers an 8x8 pixel tile
-constexpr int kWavesPerBlock = 4; // 256-thread workgroups
 
 }  // namespace ptmi

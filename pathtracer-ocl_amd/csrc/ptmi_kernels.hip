@@ -324,6 +324,15 @@ enum : int {
     F_PROJ = 16,      // not affine (see dotv): the literal double4 arithmetic, generic path only
     F_TEX = 32        // textured objects: with F_ALL | F_PROJ, the one textured instantiation
 };
+// Threads per workgroup of trace_kernel<FL>.  The BVH variants keep 4-wave groups:
+// the workgroup shares the LDS copy of the top Node4s.  The others run one wave per
+// group, so a wave that finishes its tile frees its slot (LDS included) at once
+// instead of when the slowest of four waves ends.
+#ifndef PTMI_BLOCK_NOGROUPS
+#define PTMI_BLOCK_NOGROUPS 64
+#endif
+__host__ __device__ constexpr int block_threads(int fl) { return (fl & F_GROUPS) ? 256 : PTMI_BLOCK_NOGROUPS; }
+
 
 // intersectRayWithBox (tracer.cl:270-280) returning the line's slab interval.
 // The hit decision tmin < tmax is the reference's, bit for bit.
@@ -1259,7 +1268,7 @@ template <int FL>
 #ifndef PTMI_WAVES_GROUPS
 #define PTMI_WAVES_GROUPS 3  // ... and with BVH groups (the walk needs more registers; 4 spills)
 #endif
-__global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, uint32_t s_begin, uint32_t s_end,
+__global__ __launch_bounds__(block_threads(FL), (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, uint32_t s_begin, uint32_t s_end,
                                                     uint32_t chunk_len, uint32_t tile_stride, uint32_t tile_offset,
                                                     const double* __restrict__ seeds, const double* __restrict__ sunf,
                                                     double* __restrict__ out) {
@@ -1270,7 +1279,7 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
     if constexpr ((FL & F_GROUPS) != 0 && kLdsNodes > 0) {
         const int nl = min(kLdsNodes, S.n_nodes4) * 7;
         const float4* src = reinterpret_cast<const float4*>(S.nodes4);
-        for (int k = threadIdx.x; k < nl; k += 256) node_lds4[k] = src[k];
+        for (int k = threadIdx.x; k < nl; k += block_threads(FL)) node_lds4[k] = src[k];
         __syncthreads();
     }
 #if PTMI_STATS
@@ -1280,7 +1289,7 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
     const int tiles_x = (W + kTile - 1) / kTile;
     const int tiles_y = (H + kTile - 1) / kTile;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * kWavesPerBlock + wave;
+    const int tile = blockIdx.x * (block_threads(FL) / 64) + wave;
     if (tile >= tiles_x * tiles_y) return;
     if ((uint32_t)tile % tile_stride != tile_offset) return;
     const int px = (tile % tiles_x) * kTile + (lane & 7);
@@ -1306,7 +1315,8 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
     // traversal stacks and nodes).
     constexpr int kCamComp = A ? 6 : 8;
     constexpr int kCamDepth = (FL & F_GROUPS) ? PTMI_CAM_DEPTH_GROUPS : PTMI_CAM_DEPTH;
-    __shared__ double cam_lds[kCamDepth * kCamComp * 256];
+    constexpr int kB = block_threads(FL);  // LDS stride of the per-lane camera slots
+    __shared__ double cam_lds[kCamDepth * kCamComp * kB];
     const int tid = threadIdx.x;
     // Per-lane BVH traversal stacks, lane-interleaved (entry k of lane t at
     // [k * 256 + t]) so a wave's pushes and pops hit 64 consecutive dwords.
@@ -1334,25 +1344,25 @@ __global__ __launch_bounds__(256, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAV
                                                     (int)n_gen, ro, rd);
                 int slot = hb + nb;
                 if (slot >= kCamDepth) slot -= kCamDepth;
-                double* cb = cam_lds + slot * (kCamComp * 256) + tid;
-                cb[0 * 256] = ro.x;
-                cb[1 * 256] = ro.y;
-                cb[2 * 256] = ro.z;
-                cb[3 * 256] = rd.x;
-                cb[4 * 256] = rd.y;
-                cb[5 * 256] = rd.z;
+                double* cb = cam_lds + slot * (kCamComp * kB) + tid;
+                cb[0 * kB] = ro.x;
+                cb[1 * kB] = ro.y;
+                cb[2 * kB] = ro.z;
+                cb[3 * kB] = rd.x;
+                cb[4 * kB] = rd.y;
+                cb[5 * kB] = rd.z;
                 if constexpr (!A) {
-                    cb[6 * 256] = ro.w;
-                    cb[7 * 256] = rd.w;
+                    cb[6 * kB] = ro.w;
+                    cb[7 * kB] = rd.w;
                 }
                 n_gen++;
                 nb++;
             }
         }
         if (!active && nb > 0) {
-            const double* cb = cam_lds + hb * (kCamComp * 256) + tid;
-            const d4 cro = mk(cb[0 * 256], cb[1 * 256], cb[2 * 256], A ? 1.0 : cb[6 * 256]);
-            const d4 crd = mk(cb[3 * 256], cb[4 * 256], cb[5 * 256], A ? 0.0 : cb[7 * 256]);
+            const double* cb = cam_lds + hb * (kCamComp * kB) + tid;
+            const d4 cro = mk(cb[0 * kB], cb[1 * kB], cb[2 * kB], A ? 1.0 : cb[6 * kB]);
+            const d4 crd = mk(cb[3 * kB], cb[4 * kB], cb[5 * kB], A ? 0.0 : cb[7 * kB]);
             start_path<A>(P, cro, crd);
             n_cur = n_gen - (uint32_t)nb;
             hb = (hb + 1 == kCamDepth) ? 0 : hb + 1;
@@ -1511,6 +1521,11 @@ __global__ __launch_bounds__(256) void seeds_kernel(double* __restrict__ seeds, 
 }
 
 // ---- host-side launch wrappers (called from ptmi_api.cpp) ----------------------
+int trace_block_threads(int flags) {
+    if (flags & (F_TEX | F_PROJ)) return block_threads(F_ALL | F_PROJ);
+    return block_threads(flags & F_ALL);
+}
+
 const void* trace_kernel_symbol(int flags) {
     if (flags & F_TEX) return reinterpret_cast<const void*>(&trace_kernel<F_ALL | F_PROJ | F_TEX>);
     if (flags & F_PROJ) return reinterpret_cast<const void*>(&trace_kernel<F_ALL | F_PROJ>);
@@ -1527,21 +1542,25 @@ hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, uint32_t
                         uint32_t chunk_len, uint32_t nchunks, uint32_t tile_stride, uint32_t tile_offset,
                         const double* seeds, const double* sunf, double* out, hipStream_t st) {
     const int tiles = ((S.cam.width + kTile - 1) / kTile) * ((S.cam.height + kTile - 1) / kTile);
-    dim3 grid((tiles + kWavesPerBlock - 1) / kWavesPerBlock, nchunks);
+    auto grid = [&](int fl) {
+        const int wpb = block_threads(fl) / 64;
+        return dim3((tiles + wpb - 1) / wpb, nchunks);
+    };
     if (flags & F_TEX) {  // textured scene: the generic instantiation plus the texture lookups
-        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ | F_TEX>, grid, dim3(256), 0, st, S, samples, s_begin, s_end,
+        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ | F_TEX>, grid(F_ALL | F_PROJ | F_TEX), dim3(256), 0, st, S, samples, s_begin, s_end,
                            chunk_len, tile_stride, tile_offset, seeds, sunf, out);
         return hipGetLastError();
     }
     if (flags & F_PROJ) {  // non-affine scene: one generic instantiation with the literal w arithmetic
-        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ>, grid, dim3(256), 0, st, S, samples, s_begin, s_end,
+        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ>, grid(F_ALL | F_PROJ), dim3(256), 0, st, S, samples, s_begin, s_end,
                            chunk_len, tile_stride, tile_offset, seeds, sunf, out);
         return hipGetLastError();
     }
     switch (flags & F_ALL) {
 #define K(f)                                                                                                   \
     case f:                                                                                                    \
-        hipLaunchKernelGGL(trace_kernel<f>, grid, dim3(256), 0, st, S, samples, s_begin, s_end, chunk_len,     \
+        hipLaunchKernelGGL(trace_kernel<f>, grid(f), dim3(block_threads(f)), 0, st, S, samples, s_begin, s_end, \
+                           chunk_len,                                                                          \
                            tile_stride, tile_offset, seeds, sunf, out);                                        \
         break;
         K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15)
