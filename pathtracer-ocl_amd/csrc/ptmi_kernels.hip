@@ -324,14 +324,18 @@ enum : int {
     F_PROJ = 16,      // not affine (see dotv): the literal double4 arithmetic, generic path only
     F_TEX = 32        // textured objects: with F_ALL | F_PROJ, the one textured instantiation
 };
-// Threads per workgroup of trace_kernel<FL>.  The BVH variants keep 4-wave groups:
-// the workgroup shares the LDS copy of the top Node4s.  The others run one wave per
-// group, so a wave that finishes its tile frees its slot (LDS included) at once
-// instead of when the slowest of four waves ends.
-#ifndef PTMI_BLOCK_NOGROUPS
-#define PTMI_BLOCK_NOGROUPS 64
+// Threads per workgroup of trace_kernel: one wave.  A wave that finishes its work
+// item frees its slot (LDS included) at once; with 4-wave groups the slot waited for
+// the slowest of the four (measured, 256 spp: teapot 118.9 -> 116.7 ms, gopher
+// 189.0 -> 177.1 ms, C2 236.0 -> 235.3 ms per 2048 spp).  BVH scenes then stage
+// only the top 3 levels of the traversal index per group (kLdsNodes).
+#ifndef PTMI_BLOCK
+#define PTMI_BLOCK 64
 #endif
-__host__ __device__ constexpr int block_threads(int fl) { return (fl & F_GROUPS) ? 256 : PTMI_BLOCK_NOGROUPS; }
+static constexpr int kBlock = PTMI_BLOCK;
+// Per-lane traversal stacks are lane-interleaved across the workgroup: entry k of
+// thread t at [k * kStkStride + t].
+static constexpr int kStkStride = kBlock;
 
 
 // intersectRayWithBox (tracer.cl:270-280) returning the line's slab interval.
@@ -466,7 +470,7 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 
 
 static constexpr int kStack = 24;  // per-lane LDS traversal stack (3 pushes x BVH4 depth <= 7, ptmi_bvh.cpp)
 #ifndef PTMI_LDS_NODES
-#define PTMI_LDS_NODES 120  // Node4s staged in LDS per workgroup: 4 full BVH4 levels + 35 (13.1 KB)
+#define PTMI_LDS_NODES 21  // Node4s staged in LDS per workgroup: the top 3 BVH4 levels (2.3 KB)
 #endif
 static constexpr int kLdsNodes = PTMI_LDS_NODES;
 
@@ -598,9 +602,9 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
     }
             PTMI_CX(0, 1) PTMI_CX(2, 3) PTMI_CX(0, 2) PTMI_CX(1, 3) PTMI_CX(1, 2)
 #undef PTMI_CX
-            if (k[3] < __builtin_huge_valf()) stk[(sp++) * 256] = c[3];
-            if (k[2] < __builtin_huge_valf()) stk[(sp++) * 256] = c[2];
-            if (k[1] < __builtin_huge_valf()) stk[(sp++) * 256] = c[1];
+            if (k[3] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[3];
+            if (k[2] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[2];
+            if (k[1] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[1];
             if (k[0] < __builtin_huge_valf()) {
                 cur = c[0];
                 continue;
@@ -617,7 +621,7 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
             }
         }
         if (sp == 0) break;
-        cur = stk[(--sp) * 256];
+        cur = stk[(--sp) * kStkStride];
     }
 }
 
@@ -1268,7 +1272,7 @@ template <int FL>
 #ifndef PTMI_WAVES_GROUPS
 #define PTMI_WAVES_GROUPS 3  // ... and with BVH groups (the walk needs more registers; 4 spills)
 #endif
-__global__ __launch_bounds__(block_threads(FL), (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, uint32_t s_begin, uint32_t s_end,
+__global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, uint32_t s_begin, uint32_t s_end,
                                                     uint32_t chunk_len, uint32_t tile_stride, uint32_t tile_offset,
                                                     const double* __restrict__ seeds, const double* __restrict__ sunf,
                                                     double* __restrict__ out) {
@@ -1279,7 +1283,7 @@ __global__ __launch_bounds__(block_threads(FL), (FL & F_GROUPS) ? PTMI_WAVES_GRO
     if constexpr ((FL & F_GROUPS) != 0 && kLdsNodes > 0) {
         const int nl = min(kLdsNodes, S.n_nodes4) * 7;
         const float4* src = reinterpret_cast<const float4*>(S.nodes4);
-        for (int k = threadIdx.x; k < nl; k += block_threads(FL)) node_lds4[k] = src[k];
+        for (int k = threadIdx.x; k < nl; k += kBlock) node_lds4[k] = src[k];
         __syncthreads();
     }
 #if PTMI_STATS
@@ -1289,7 +1293,7 @@ __global__ __launch_bounds__(block_threads(FL), (FL & F_GROUPS) ? PTMI_WAVES_GRO
     const int tiles_x = (W + kTile - 1) / kTile;
     const int tiles_y = (H + kTile - 1) / kTile;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * (block_threads(FL) / 64) + wave;
+    const int tile = blockIdx.x * (kBlock / 64) + wave;
     if (tile >= tiles_x * tiles_y) return;
     if ((uint32_t)tile % tile_stride != tile_offset) return;
     const int px = (tile % tiles_x) * kTile + (lane & 7);
@@ -1315,12 +1319,12 @@ __global__ __launch_bounds__(block_threads(FL), (FL & F_GROUPS) ? PTMI_WAVES_GRO
     // traversal stacks and nodes).
     constexpr int kCamComp = A ? 6 : 8;
     constexpr int kCamDepth = (FL & F_GROUPS) ? PTMI_CAM_DEPTH_GROUPS : PTMI_CAM_DEPTH;
-    constexpr int kB = block_threads(FL);  // LDS stride of the per-lane camera slots
+    constexpr int kB = kBlock;  // LDS stride of the per-lane camera slots
     __shared__ double cam_lds[kCamDepth * kCamComp * kB];
     const int tid = threadIdx.x;
     // Per-lane BVH traversal stacks, lane-interleaved (entry k of lane t at
-    // [k * 256 + t]) so a wave's pushes and pops hit 64 consecutive dwords.
-    __shared__ int stk_lds[(FL & F_GROUPS) ? kStack * 256 : 1];
+    // [k * kStkStride + t]) so a wave's pushes and pops hit 64 consecutive dwords.
+    __shared__ int stk_lds[(FL & F_GROUPS) ? kStack * kStkStride : 1];
     int* stk = (FL & F_GROUPS) ? stk_lds + tid : nullptr;
     uint32_t n_gen = c0;  // next sample whose camera ray is to be generated
     uint32_t n_cur = 0;
@@ -1521,10 +1525,7 @@ __global__ __launch_bounds__(256) void seeds_kernel(double* __restrict__ seeds, 
 }
 
 // ---- host-side launch wrappers (called from ptmi_api.cpp) ----------------------
-int trace_block_threads(int flags) {
-    if (flags & (F_TEX | F_PROJ)) return block_threads(F_ALL | F_PROJ);
-    return block_threads(flags & F_ALL);
-}
+int trace_block_threads(int) { return kBlock; }
 
 const void* trace_kernel_symbol(int flags) {
     if (flags & F_TEX) return reinterpret_cast<const void*>(&trace_kernel<F_ALL | F_PROJ | F_TEX>);
@@ -1542,25 +1543,22 @@ hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, uint32_t
                         uint32_t chunk_len, uint32_t nchunks, uint32_t tile_stride, uint32_t tile_offset,
                         const double* seeds, const double* sunf, double* out, hipStream_t st) {
     const int tiles = ((S.cam.width + kTile - 1) / kTile) * ((S.cam.height + kTile - 1) / kTile);
-    auto grid = [&](int fl) {
-        const int wpb = block_threads(fl) / 64;
-        return dim3((tiles + wpb - 1) / wpb, nchunks);
-    };
+    constexpr int wpb = kBlock / 64;
+    const dim3 grid((tiles + wpb - 1) / wpb, nchunks);
     if (flags & F_TEX) {  // textured scene: the generic instantiation plus the texture lookups
-        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ | F_TEX>, grid(F_ALL | F_PROJ | F_TEX), dim3(256), 0, st, S, samples, s_begin, s_end,
+        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ | F_TEX>, grid, dim3(kBlock), 0, st, S, samples, s_begin, s_end,
                            chunk_len, tile_stride, tile_offset, seeds, sunf, out);
         return hipGetLastError();
     }
     if (flags & F_PROJ) {  // non-affine scene: one generic instantiation with the literal w arithmetic
-        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ>, grid(F_ALL | F_PROJ), dim3(256), 0, st, S, samples, s_begin, s_end,
+        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ>, grid, dim3(kBlock), 0, st, S, samples, s_begin, s_end,
                            chunk_len, tile_stride, tile_offset, seeds, sunf, out);
         return hipGetLastError();
     }
     switch (flags & F_ALL) {
 #define K(f)                                                                                                   \
     case f:                                                                                                    \
-        hipLaunchKernelGGL(trace_kernel<f>, grid(f), dim3(block_threads(f)), 0, st, S, samples, s_begin, s_end, \
-                           chunk_len,                                                                          \
+        hipLaunchKernelGGL(trace_kernel<f>, grid, dim3(kBlock), 0, st, S, samples, s_begin, s_end, chunk_len,  \
                            tile_stride, tile_offset, seeds, sunf, out);                                        \
         break;
         K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15)
