@@ -1,19 +1,41 @@
 """Summarise a tools/profile_round.sh output directory into profiles/<round>/:
-kernel_stats_<cfg>.csv, bench_<cfg>.json, pmc_c2*.{csv,json} and SUMMARY.md.
-    python tools/profile_summary.py gpurun_out/prof_r1b profiles/r1
+kernel_stats_<cfg>.csv, bench_<cfg>.json, pmc_c2*.{csv,json} and SUMMARY.md, plus
+the derived VALU metrics of tools/pmc.sh output directories given as cfg=dir.
+    python tools/profile_summary.py gpurun_out/prof_r1b profiles/r1 [c2=gpurun_out/pmc_c2 ...]
 """
 import csv
 import json
 import os
+import re
 import shutil
 import sys
+
+F64 = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")
+
+
+def valu_metrics(summary_txt):
+    """VALU-active fraction, resident waves per SIMD, lane utilisation and FP64 share
+    of one trace_kernel launch from tools/pmc.sh's summary (MI355X: 8 XCDs x 32 CUs x
+    4 SIMDs; SQ_*_CYCLES count quad-cycles, GRBM_GUI_ACTIVE is summed over XCDs)."""
+    v = {}
+    with open(summary_txt) as f:
+        for line in f:
+            m = re.match(r"(\w+)\s+([\d.]+)\s+\(dispatches", line)
+            if m:
+                v[m.group(1)] = float(m.group(2))
+    simd_cycles = 256 * 4 * v["GRBM_GUI_ACTIVE"] / 8
+    return {"valu_active": 4 * v["SQ_ACTIVE_INST_VALU"] / simd_cycles,
+            "waves_per_simd": 4 * v["SQ_WAVE_CYCLES"] / simd_cycles,
+            "lane_util": v["SQ_THREAD_CYCLES_VALU"] / (64 * v["SQ_ACTIVE_INST_VALU"]),
+            "fp64_share": sum(v.get(k, 0.0) for k in F64) / v["SQ_INSTS_VALU"],
+            "valu_insts_per_wave": v["SQ_INSTS_VALU"] / v["SQ_WAVES"]}
 
 CMDS = {"c2": "python3 bench.py --config c2 --steps 2 --warmup 1",
         "c4": "python3 bench.py --config c4 --samples 256 --steps 1 --warmup 1 --no-cpu-baseline --no-trace-call",
         "c5": "python3 bench.py --config c5 --samples 256 --steps 1 --warmup 1 --no-cpu-baseline --no-trace-call"}
 
 
-def main(src, dst):
+def main(src, dst, pmc_dirs=()):
     os.makedirs(dst, exist_ok=True)
     lines = ["# rocprofv3 --kernel-trace --stats summaries (tools/profile_round.sh, one MI355X)", ""]
     for c, cmd in CMDS.items():
@@ -54,10 +76,21 @@ def main(src, dst):
                      "WRITE_SIZE %.1f KB -> %.1f MB per launch" % (cfg, what, p["fetch_size_kb_raw_per_launch"],
                                                                  p["write_size_kb_per_launch"],
                                                                  p["hbm_bytes_per_launch"] / 1e6))
+    if pmc_dirs:
+        lines += ["", "## trace_kernel VALU counters (tools/pmc.sh, separate --pmc passes; c2 one 2048-spp frame,"
+                  " c4 / c5 one 256-spp frame)", "",
+                  "| config | VALU active | resident waves/SIMD | VALU lane utilisation | FP64 share of VALU insts |",
+                  "|---|---|---|---|---|"]
+    for arg in pmc_dirs:
+        cfg, d = arg.split("=", 1)
+        shutil.copy(os.path.join(d, "summary.txt"), os.path.join(dst, "pmc_valu_%s.txt" % cfg))
+        m = valu_metrics(os.path.join(d, "summary.txt"))
+        lines.append("| %s | %.3f | %.2f | %.3f | %.3f |" % (cfg, m["valu_active"], m["waves_per_simd"],
+                                                            m["lane_util"], m["fp64_share"]))
     with open(os.path.join(dst, "SUMMARY.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3:])
