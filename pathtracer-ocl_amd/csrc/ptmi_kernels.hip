@@ -15,6 +15,7 @@
 
 #include "ptmi_device.h"
 #include "ptmi_sinf.h"
+#include "ptmi_fp64core.h"
 
 // PTMI_ABLATE: DIAGNOSTIC builds only (make ablate) -- removes a component to
 // measure its share of the run time.  Images from such builds are wrong by
@@ -171,7 +172,8 @@ __device__ __noinline__ d4 normalize3(double x, double y, double z) {
             d = fma(pz, pz, fma(py, py, px * px));
         }
     }
-    const double s = (PTMI_ABLATE & 256) ? __builtin_amdgcn_rsq(d) : rsqrt(d);  // DIAGNOSTIC 256
+    // d is a positive normal here (zero returned above, tiny / huge rescaled): rsqrt's core
+    const double s = (PTMI_ABLATE & 256) ? __builtin_amdgcn_rsq(d) : rsqrt_core(d);  // DIAGNOSTIC 256
     return mk(px * s, py * s, pz * s, 0.0);
 }
 template <bool A>
@@ -645,16 +647,27 @@ __device__ __forceinline__ void sphere_quad(d4 o, d4 d, double& a, double& b, do
     disc = (b * b) - 4 * a * c;
 }
 // ... and its roots.
+// Affine (A): sqrt / divide cores.  In a tame scene (ptmi_api.cpp) 2a >= 2^-500 for
+// every ray, so a root that can be a candidate (EPSILON < t <= 1024) has a quotient
+// and operands inside the cores' range; a root outside it is below EPSILON, above
+// 1024 or NaN under both arithmetics, so the candidate set and the t1 > EPSILON
+// branch are the same.  disc > 0 is a difference of two doubles, so it is either
+// >= 2^-767 or so small that b is too (then both roots are below EPSILON).
+template <bool A>
 __device__ __forceinline__ void sphere_roots(Hit& h, double a, double b, double disc, int slot, int key) {
     if (disc > 0.0) {
         // a > 0 and sq >= 0 give t1 <= t2 after rounding (rounding is monotonic),
         // so t2 can only be recorded as the winner when t1 itself is not a
         // candidate (t1 <= EPSILON); a tie t2 == t1 never replaces t1.
-        double sq = (PTMI_ABLATE & 128) ? __builtin_amdgcn_sqrt(disc) : sqrt(disc);  // DIAGNOSTIC 128
-        double t1 = (PTMI_ABLATE & 128) ? (-b - sq) * __builtin_amdgcn_rcp(2 * a) : (-b - sq) / (2 * a);
+        double sq = (PTMI_ABLATE & 128) ? __builtin_amdgcn_sqrt(disc) : A ? sqrt_core(disc) : sqrt(disc);  // DIAGNOSTIC 128
+        double t1 = (PTMI_ABLATE & 128) ? (-b - sq) * __builtin_amdgcn_rcp(2 * a)
+                    : A                 ? div_core(-b - sq, 2 * a)
+                                        : (-b - sq) / (2 * a);
         consider_sel(h, t1, slot, key);
         if (!(t1 > kEps)) {
-            double t2 = (PTMI_ABLATE & 128) ? (-b + sq) * __builtin_amdgcn_rcp(2 * a) : (-b + sq) / (2 * a);
+            double t2 = (PTMI_ABLATE & 128) ? (-b + sq) * __builtin_amdgcn_rcp(2 * a)
+                        : A                 ? div_core(-b + sq, 2 * a)
+                                            : (-b + sq) / (2 * a);
             consider_sel(h, t2, slot, key);
         }
     }
@@ -663,7 +676,7 @@ template <bool A>
 __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int key) {
     double a, b, disc;
     sphere_quad<A>(o, d, a, b, disc);
-    sphere_roots(h, a, b, disc, slot, key);
+    sphere_roots<A>(h, a, b, disc, slot, key);
 }
 
 // findClosestIntersection (tracer.cl:537-742), one loop per object type.  Loop
@@ -684,7 +697,11 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         const double oy = ((P.row1[0] * ro.x + P.row1[1] * ro.y) + P.row1[2] * ro.z) + (A ? P.row1[3] : P.row1[3] * ro.w);
         const double dy0 = (P.row1[0] * rd.x + P.row1[1] * rd.y) + P.row1[2] * rd.z;
         const double dy = A ? dy0 : dy0 + P.row1[3] * rd.w;
-        q = (PTMI_ABLATE & 64) ? -oy * __builtin_amdgcn_rcp(dy) : -oy / dy;  // DIAGNOSTIC 64
+        // Affine: the divide core.  Its range steps act only when |dy| is denormal or
+        // above 2^1022, -oy is below 2^-970, or the quotient is denormal or above 2^767;
+        // then q <= EPSILON, |dy| <= EPSILON, or q >= 1024 under both arithmetics, and
+        // the plane is not taken either way.
+        q = (PTMI_ABLATE & 64) ? -oy * __builtin_amdgcn_rcp(dy) : A ? div_core(-oy, dy) : -oy / dy;  // DIAGNOSTIC 64
         ok = (fabs(dy) > kEps) & (q > kEps);
     };
     auto plane_take = [&](const PlaneRec& P, double q, bool ok) {
@@ -729,8 +746,8 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         double a0, b0, disc0, a1, b1, disc1;
         sphere_quad<A>(o0, d0, a0, b0, disc0);
         sphere_quad<A>(o1, d1, a1, b1, disc1);
-        sphere_roots(h, a0, b0, disc0, Q0.slot, Q0.key);
-        sphere_roots(h, a1, b1, disc1, Q1.slot, Q1.key);
+        sphere_roots<A>(h, a0, b0, disc0, Q0.slot, Q0.key);
+        sphere_roots<A>(h, a1, b1, disc1, Q1.slot, Q1.key);
     }
     if (q < nq) {
         const SphereRec Q0 = S.spheres[q];
@@ -909,7 +926,9 @@ template <bool A>
 __device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float fz) {
     double rand1 = 2.0 * kPi * (double)noise3d(fx, fy, fz);
     double rand2 = (double)noise3d(fy, fz, fx);
-    double rand2s = sqrt(rand2);
+    // Affine: sqrt's core; rand2 is 0 or a float >= 2^-149, so in its range (and 1 - rand2
+    // is in (0, 1]), sqrt(+0) = +0 kept by the select.
+    double rand2s = A ? (rand2 == 0.0 ? 0.0 : sqrt_core(rand2)) : sqrt(rand2);
     // cross(axis, n) for a unit axis: the fma chains of opencl.bc's cross reduce
     // exactly (up to the sign of exact zeros) to component moves:
     //   cross((0,1,0,0), n) = (n.z, 0, -n.x, 0),  cross((1,0,0,0), n) = (0, -n.z, n.y, 0)
@@ -923,7 +942,8 @@ __device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float
     } else {
         sincos(rand1, &sr, &cr);  // ocml sincos == (sin, cos) bit-for-bit: one shared reduction
     }
-    return add4(add4(scl4(scl4(u, cr), rand2s), scl4(scl4(v, sr), rand2s)), scl4(nv, sqrt(1.0 - rand2)));
+    const double rc = A ? sqrt_core(1.0 - rand2) : sqrt(1.0 - rand2);
+    return add4(add4(scl4(scl4(u, cr), rand2s), scl4(scl4(v, sr), rand2s)), scl4(nv, rc));
 }
 
 // sunflower (tracer.cl:221-248), randomize == false.

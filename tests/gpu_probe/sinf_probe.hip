@@ -9,6 +9,7 @@
 #define PT_FN __host__ __device__ static inline
 #include "../../oracle/ocml_sinf.h"
 #include "../../pathtracer-ocl_amd/csrc/ptmi_sinf.h"  // the product's noise sin (kernel code)
+#include "../../pathtracer-ocl_amd/csrc/ptmi_fp64core.h"  // the product's divide / sqrt / rsqrt cores
 
 __global__ void sinf_check(uint64_t base, uint64_t count, unsigned long long* mism, unsigned int* first) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -39,6 +40,42 @@ __global__ void ptmi_sinf_check(uint64_t base, uint64_t count, unsigned long lon
         atomicAdd(mism, 1ull);
         atomicMin(first, bits);
     }
+}
+
+// Random doubles with a uniform exponent in [emin, emax], random mantissa and sign.
+__device__ static inline uint64_t splitmix(uint64_t& z) {
+    z += 0x9E3779B97F4A7C15ull;
+    uint64_t r = z;
+    r = (r ^ (r >> 30)) * 0xBF58476D1CE4E5B9ull;
+    r = (r ^ (r >> 27)) * 0x94D049BB133111EBull;
+    return r ^ (r >> 31);
+}
+__device__ static inline double rand_double(uint64_t& z, int emin, int emax, bool sign) {
+    const uint64_t u = splitmix(z);
+    const int e = emin + (int)(splitmix(z) % (uint64_t)(emax - emin + 1));
+    const uint64_t bits = ((uint64_t)(e + 1023) << 52) | (u & 0xFFFFFFFFFFFFFull) | (sign ? (u & (1ull << 63)) : 0ull);
+    return __longlong_as_double((long long)bits);
+}
+// ptmi::div_core / sqrt_core / rsqrt_core against the compiler's operators on the
+// ranges the kernel relies on: quotients of operands in [2^-500, 2^500]; sqrt of
+// [2^-767, 2^1023]; rsqrt of normal [2^-1022, 2^1023].  mism[k] counts op k.
+__global__ void fp64core_check(uint64_t seed, uint64_t per_thread, unsigned long long* mism) {
+    uint64_t z = seed ^ ((uint64_t)(blockIdx.x * blockDim.x + threadIdx.x) * 0xD1B54A32D192ED03ull);
+    unsigned long long m0 = 0, m1 = 0, m2 = 0;
+    for (uint64_t k = 0; k < per_thread; k++) {
+        const double x = rand_double(z, -500, 500, true), y = rand_double(z, -500, 500, true);
+        const double q0 = x / y, q1 = ptmi::div_core(x, y);
+        m0 += __double_as_longlong(q0) != __double_as_longlong(q1);
+        const double s = rand_double(z, -767, 1022, false);
+        const double s0 = sqrt(s), s1 = ptmi::sqrt_core(s);
+        m1 += __double_as_longlong(s0) != __double_as_longlong(s1);
+        const double r = rand_double(z, -1022, 1022, false);
+        const double r0 = rsqrt(r), r1 = ptmi::rsqrt_core(r);
+        m2 += __double_as_longlong(r0) != __double_as_longlong(r1);
+    }
+    if (m0) atomicAdd(&mism[0], m0);
+    if (m1) atomicAdd(&mism[1], m1);
+    if (m2) atomicAdd(&mism[2], m2);
 }
 
 __global__ void sinf_eval(const float* in, float* out, uint64_t n) {
@@ -81,6 +118,19 @@ extern "C" int probe_ptmi_sinf_all(unsigned long long* mismatches, unsigned int*
     (void)hipMemcpy(first_bad, df, 4, hipMemcpyDeviceToHost);
     (void)hipFree(dm);
     (void)hipFree(df);
+    return 0;
+}
+
+extern "C" int probe_fp64core(uint64_t seed, uint64_t total, unsigned long long* mismatches3) {
+    unsigned long long* dm;
+    if (hipMalloc(&dm, 24)) return -1;
+    (void)hipMemset(dm, 0, 24);
+    const uint64_t threads = 1ull << 20, per = (total + threads - 1) / threads;
+    hipLaunchKernelGGL(fp64core_check, dim3((unsigned)(threads / 256)), dim3(256), 0, 0, seed, per, dm);
+    if (hipGetLastError() != hipSuccess) return -2;
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    (void)hipMemcpy(mismatches3, dm, 24, hipMemcpyDeviceToHost);
+    (void)hipFree(dm);
     return 0;
 }
 

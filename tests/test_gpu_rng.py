@@ -21,6 +21,7 @@ def _lib():
     lib = ctypes.CDLL(LIB)
     lib.probe_sinf_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
     lib.probe_ptmi_sinf_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
+    lib.probe_fp64core.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_ulonglong)]
     lib.probe_sinf_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     return lib
 
@@ -40,6 +41,16 @@ def test_kernel_sinf_bit_identical_below_2p19():
     m, f = ctypes.c_ulonglong(), ctypes.c_uint()
     assert lib.probe_ptmi_sinf_all(ctypes.byref(m), ctypes.byref(f)) == 0
     assert m.value == 0, "%d mismatches, first input bits 0x%08x" % (m.value, f.value)
+
+
+def test_fp64_cores_match_compiler_operators():
+    """csrc/ptmi_fp64core.h: the divide / sqrt / rsqrt cores the affine kernels use
+    return the bits of the compiler's x / y, sqrt and rsqrt on their ranges (2^28
+    random operands per operation, uniform exponents, random mantissas)."""
+    lib = _lib()
+    m = (ctypes.c_ulonglong * 3)()
+    assert lib.probe_fp64core(12345, 1 << 28, m) == 0
+    assert list(m) == [0, 0, 0], "mismatches (div, sqrt, rsqrt): %s" % list(m)
 
 
 def test_cpu_restatement_replays_gpu_ocml():
