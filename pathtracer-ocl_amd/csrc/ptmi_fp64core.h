@@ -2,6 +2,7 @@
 // rsqrt for gfx950, without their range steps (used by ptmi_kernels.hip's affine
 // instantiations; checked against the operators by tests/test_gpu_rng.py).
 #pragma once
+#include <stdint.h>
 
 namespace ptmi {
 
@@ -45,6 +46,54 @@ __device__ __forceinline__ double rsqrt_core(double x) {  // ocml rsqrt_f64 for 
     const double t = r * e;
     e = fma(e, 0.375, 0.5);
     return fma(t, e, r);
+}
+
+// ocml's __ocml_sincos_f64 for 0 <= x < 1024 (ROCm 7.2 ocml.bc, read off the IR):
+// __ocmlpriv_trigredsmall_f64 (Cody-Waite with a double-double remainder), then
+// __ocmlpriv_sincosred2_f64 and the quadrant swap.  Left out, being identities on
+// this domain: the large-argument branch (x >= 2^30), the sign of x (+0), the
+// non-finite fix-up, and the error term fma(k, pio2_m, -k * pio2_m), which is +0
+// because pio2_m has 43 significant bits and k = rint(x * 2/pi) < 2^10.
+__device__ __forceinline__ void sincos_core(double x, double* sp, double* cp) {
+    const double dn = __builtin_rint(x * __builtin_bit_cast(double, 0x3FE45F306DC9C883ull));
+    const double t4 = fma(dn, __builtin_bit_cast(double, 0xBFF921FB54442D18ull), x);
+    const double t5 = fma(dn, __builtin_bit_cast(double, 0xBC91A62633145C00ull), t4);
+    const double t6 = dn * __builtin_bit_cast(double, 0x3C91A62633145C00ull);
+    const double t9 = t4 - t6;
+    const double t10 = t4 - t9;
+    const double t11 = t10 - t6;
+    const double t12 = t9 - t5;
+    const double t13 = t12 + t11;
+    const double t15 = fma(dn, __builtin_bit_cast(double, 0xB97B839A252049C0ull), t13);
+    const double rh = t5 + t15;
+    const double rl = t15 - (rh - t5);
+    const int q = ((int)dn) & 3;
+    // __ocmlpriv_sincosred2_f64(rh, rl)
+    const double x2 = rh * rh;
+    const double hx = x2 * 0.5;
+    const double c0 = 1.0 - hx;
+    const double c1 = (1.0 - c0) - hx;
+    const double x4 = x2 * x2;
+    double pc = fma(x2, __builtin_bit_cast(double, 0xBDA907DB46CC5E42ull), __builtin_bit_cast(double, 0x3E21EEB69037AB78ull));
+    pc = fma(x2, pc, __builtin_bit_cast(double, 0xBE927E4FA17F65F6ull));
+    pc = fma(x2, pc, __builtin_bit_cast(double, 0x3EFA01A019F4EC90ull));
+    pc = fma(x2, pc, __builtin_bit_cast(double, 0xBF56C16C16C16967ull));
+    pc = fma(x2, pc, __builtin_bit_cast(double, 0x3FA5555555555555ull));
+    const double cc = c0 + fma(x4, pc, fma(rh, -rl, c1));
+    double ps = fma(x2, __builtin_bit_cast(double, 0x3DE5E0B2F9A43BB8ull), __builtin_bit_cast(double, 0xBE5AE600B42FDFA7ull));
+    ps = fma(x2, ps, __builtin_bit_cast(double, 0x3EC71DE3796CDE01ull));
+    ps = fma(x2, ps, __builtin_bit_cast(double, 0xBF2A01A019E83E5Cull));
+    ps = fma(x2, ps, __builtin_bit_cast(double, 0x3F81111111110BB3ull));
+    const double x3 = rh * -x2;
+    const double s1 = fma(x3, ps, rl * 0.5);
+    const double s2 = fma(x2, s1, -rl);
+    const double ss = rh - fma(x3, __builtin_bit_cast(double, 0xBFC5555555555555ull), s2);
+    // __ocml_sincos_f64: quadrant swap and sign flips (x >= 0)
+    const uint64_t flip = (q > 1) ? 0x8000000000000000ull : 0ull;
+    const double sv = (q & 1) ? cc : ss;
+    const double cv = (q & 1) ? -ss : cc;
+    *sp = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, sv) ^ flip);
+    *cp = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, cv) ^ flip);
 }
 
 }  // namespace ptmi

@@ -939,6 +939,8 @@ __device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float
     if (PTMI_ABLATE & 4) {
         cr = 1.0 - rand1 * 0.1;
         sr = rand1 * 0.15;
+    } else if constexpr (A) {
+        sincos_core(rand1, &sr, &cr);  // rand1 in [0, 2 pi): ocml's sincos without its range steps
     } else {
         sincos(rand1, &sr, &cr);  // ocml sincos == (sin, cos) bit-for-bit: one shared reduction
     }

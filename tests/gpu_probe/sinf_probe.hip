@@ -78,6 +78,23 @@ __global__ void fp64core_check(uint64_t seed, uint64_t per_thread, unsigned long
     if (m2) atomicAdd(&mism[2], m2);
 }
 
+// ptmi::sincos_core against ocml's sincos for the hemisphere angle of every noise
+// value: rand1 = 2 * (double)3.14159265359f * (double)v for each float v in [0, 1)
+// (tracer.cl:349, as ptmi_kernels.hip random_hemisphere computes it).
+__global__ void sincos_check(unsigned long long* mism, unsigned int* first) {
+    const uint32_t bits = blockIdx.x * blockDim.x + threadIdx.x;
+    if (bits >= 0x3F800000u) return;
+    const double kpi = (double)3.14159265359f;
+    const double x = 2.0 * kpi * (double)pto_bits2f(bits);
+    double s0, c0, s1, c1;
+    sincos(x, &s0, &c0);
+    ptmi::sincos_core(x, &s1, &c1);
+    if (__double_as_longlong(s0) != __double_as_longlong(s1) || __double_as_longlong(c0) != __double_as_longlong(c1)) {
+        atomicAdd(mism, 1ull);
+        atomicMin(first, bits);
+    }
+}
+
 __global__ void sinf_eval(const float* in, float* out, uint64_t n) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = sinf(in[i]);
@@ -131,6 +148,22 @@ extern "C" int probe_fp64core(uint64_t seed, uint64_t total, unsigned long long*
     if (hipDeviceSynchronize() != hipSuccess) return -3;
     (void)hipMemcpy(mismatches3, dm, 24, hipMemcpyDeviceToHost);
     (void)hipFree(dm);
+    return 0;
+}
+
+extern "C" int probe_sincos_core_all(unsigned long long* mismatches, unsigned int* first_bad) {
+    unsigned long long* dm;
+    unsigned int* df;
+    if (hipMalloc(&dm, 8) || hipMalloc(&df, 4)) return -1;
+    (void)hipMemset(dm, 0, 8);
+    (void)hipMemset(df, 0xff, 4);
+    hipLaunchKernelGGL(sincos_check, dim3(0x3F800000u / 256), dim3(256), 0, 0, dm, df);
+    if (hipGetLastError() != hipSuccess) return -2;
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    (void)hipMemcpy(mismatches, dm, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(first_bad, df, 4, hipMemcpyDeviceToHost);
+    (void)hipFree(dm);
+    (void)hipFree(df);
     return 0;
 }
 

@@ -22,6 +22,7 @@ def _lib():
     lib.probe_sinf_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
     lib.probe_ptmi_sinf_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
     lib.probe_fp64core.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_ulonglong)]
+    lib.probe_sincos_core_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
     lib.probe_sinf_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     return lib
 
@@ -51,6 +52,15 @@ def test_fp64_cores_match_compiler_operators():
     m = (ctypes.c_ulonglong * 3)()
     assert lib.probe_fp64core(12345, 1 << 28, m) == 0
     assert list(m) == [0, 0, 0], "mismatches (div, sqrt, rsqrt): %s" % list(m)
+
+
+def test_sincos_core_bit_identical_every_hemisphere_angle():
+    """csrc/ptmi_fp64core.h sincos_core (ocml's sincos_f64 without its range steps)
+    equals ocml's sincos for rand1 = 2 pi v at every float noise value v in [0, 1)."""
+    lib = _lib()
+    m, f = ctypes.c_ulonglong(), ctypes.c_uint()
+    assert lib.probe_sincos_core_all(ctypes.byref(m), ctypes.byref(f)) == 0
+    assert m.value == 0, "%d mismatches, first noise bits 0x%08x" % (m.value, f.value)
 
 
 def test_cpu_restatement_replays_gpu_ocml():
