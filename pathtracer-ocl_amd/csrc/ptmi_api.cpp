@@ -325,16 +325,20 @@ int ptmi_scene_create_textured(int device_index, const void* objects, uint32_t n
     // far above the denormal range for every unit-scale ray direction d: each sphere's
     // inverse has linear-part entries <= 2^64 and |det| >= 2^-64, so its smallest singular
     // value is >= 2^-196.  Scenes outside that take the generic instantiation.
-    for (const DevObject& o : objs) {
-        if (o.type != 1) continue;
-        const double* m = o.inv;
+    // The same bound on the camera inverse keeps |pixel - origin| >= 2^-196 for its
+    // normalize's core, and on sphere inverses (through their transposes) keeps sphere
+    // normals >= 2^-196 long.
+    auto tame = [](const double* m) {
         double mx = 0.0;
         for (int r = 0; r < 3; r++)
             for (int c = 0; c < 3; c++) mx = std::max(mx, std::fabs(m[4 * r + c]));
         const double det = m[0] * (m[5] * m[10] - m[6] * m[9]) - m[1] * (m[4] * m[10] - m[6] * m[8]) +
                            m[2] * (m[4] * m[9] - m[5] * m[8]);
-        affine = affine && mx <= 0x1p64 && std::fabs(det) >= 0x1p-64;
-    }
+        return mx <= 0x1p64 && std::fabs(det) >= 0x1p-64;
+    };
+    affine = affine && tame(cam.inv);
+    for (const DevObject& o : objs)
+        if (o.type == 1) affine = affine && tame(o.inv);
     if (!affine) flags |= 16;                                           // F_PROJ
     // Textured plane/sphere/cube colours or plane normal maps: the one textured
     // instantiation (generic arithmetic + software sampler, tracer.cl:907-914, 1077-1092).

@@ -176,6 +176,15 @@ __device__ __noinline__ d4 normalize3(double x, double y, double z) {
     const double s = (PTMI_ABLATE & 256) ? __builtin_amdgcn_rsq(d) : rsqrt_core(d);  // DIAGNOSTIC 256
     return mk(px * s, py * s, pz * s, 0.0);
 }
+// normalize3's main path alone -- for vectors whose squared length is known to be a
+// positive normal double, where the zero test and the rescaling branches are identities.
+__device__ __forceinline__ d4 norm3_core(d4 v) {
+    double d = v.x * v.x;
+    d = fma(v.y, v.y, d);
+    d = fma(v.z, v.z, d);
+    const double s = rsqrt_core(d);
+    return mk(v.x * s, v.y * s, v.z * s, 0.0);
+}
 template <bool A>
 __device__ __forceinline__ d4 normv(d4 v) {
     if constexpr (A) return normalize3(v.x, v.y, v.z);
@@ -933,7 +942,8 @@ __device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float
     // exactly (up to the sign of exact zeros) to component moves:
     //   cross((0,1,0,0), n) = (n.z, 0, -n.x, 0),  cross((1,0,0,0), n) = (0, -n.z, n.y, 0)
     d4 c = fabs(nv.x) > 0.1 ? mk(nv.z, 0.0, -nv.x, 0.0) : mk(0.0, -nv.z, nv.y, 0.0);
-    d4 u = normv<A>(c);
+    // |c|^2 >= 0.01 for a unit normal (|n.x| > 0.1 or n.y^2 + n.z^2 >= 0.99): normalize's core
+    d4 u = A ? norm3_core(c) : normv<A>(c);
     d4 v = cross4(nv, u);
     double sr, cr;
     if (PTMI_ABLATE & 4) {
@@ -985,7 +995,9 @@ __device__ __forceinline__ void ray_for_pixel(const DevCamera& cam, const double
                   A ? 1.0 : ((m[12] * a + m[13] * b) + (-m[14])) + m[15]);
     d4 origin = ld4(cam.origin);
     if (A) origin.w = 1.0;
-    d4 dir = (PTMI_ABLATE & 2) ? sub4(pixel, origin) : normv<A>(sub4(pixel, origin));
+    // Affine scenes have a tame camera (ptmi_api.cpp): |pixel - origin| >= 2^-196, so
+    // normalize's core.
+    d4 dir = (PTMI_ABLATE & 2) ? sub4(pixel, origin) : A ? norm3_core(sub4(pixel, origin)) : normv<A>(sub4(pixel, origin));
     if (kDof && cam.aperture != 0) {
         d4 pos = add4(origin, scl4(dir, cam.focal_length));
         const double sx = sunf[2 * sample], sy = sunf[2 * sample + 1];
@@ -1015,7 +1027,9 @@ struct PathState {
     bool dead;
 };
 
-template <bool A>
+// `dead` is a shortcut only (a NaN path misses and adds 0 either way), taken where
+// NaN camera rays occur: DoF scenes.
+template <bool A, bool kDof>
 __device__ __forceinline__ void start_path(PathState& P, d4 ro, d4 rd) {
     P.ro = ro;
     P.rd = rd;
@@ -1023,8 +1037,8 @@ __device__ __forceinline__ void start_path(PathState& P, d4 ro, d4 rd) {
     P.ar = P.ag = P.ab = 0.0;
     P.b = P.k = P.effective = 0;
     P.inside = P.done = false;
-    P.dead = !(isfinite(ro.x) && isfinite(ro.y) && isfinite(ro.z) && (A || isfinite(ro.w)) && isfinite(rd.x) &&
-               isfinite(rd.y) && isfinite(rd.z) && (A || isfinite(rd.w)));
+    P.dead = kDof && !(isfinite(ro.x) && isfinite(ro.y) && isfinite(ro.z) && (A || isfinite(ro.w)) &&
+                       isfinite(rd.x) && isfinite(rd.y) && isfinite(rd.z) && (A || isfinite(rd.w)));
 }
 
 // ---- Textures (tracer.cl:113-213, 829, 907-914, 1077-1092) ----------------------
@@ -1203,7 +1217,10 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
             }
             nv.w = 0.0;
         }
-        nv = normv<A>(nv);
+        // A sphere's normal invT * (a point on the unit sphere) has |nv| >= 2^-196 in a tame
+        // scene (ptmi_api.cpp): normalize's core.  Other shapes keep the full normalize.
+        if (A && type == 1) nv = norm3_core(nv);
+        else nv = normv<A>(nv);
     }
     if (dotv<A>(eye, nv) < 0.0) nv = scl4(nv, -1.0);
     d4 over = add4(pos, scl4(nv, kEps));
@@ -1389,7 +1406,7 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
             const double* cb = cam_lds + hb * (kCamComp * kB) + tid;
             const d4 cro = mk(cb[0 * kB], cb[1 * kB], cb[2 * kB], A ? 1.0 : cb[6 * kB]);
             const d4 crd = mk(cb[3 * kB], cb[4 * kB], cb[5 * kB], A ? 0.0 : cb[7 * kB]);
-            start_path<A>(P, cro, crd);
+            start_path<A, (FL & F_DOF) != 0>(P, cro, crd);
             n_cur = n_gen - (uint32_t)nb;
             hb = (hb + 1 == kCamDepth) ? 0 : hb + 1;
             nb--;
