@@ -106,6 +106,26 @@ def test_affine_cores_match_generic_large(monkeypatch, scene, ap):
     assert np.array_equal(spec, gen)
 
 
+def test_untame_scene_matches_cpu_oracle():
+    """A sphere scaled by 2^-70 (inverse entries 2^70, outside the tame-scene bound of
+    ptmi_api.cpp) sends the scene to the generic instantiation with the compiler's full
+    divide / sqrt / normalize expansions; the image still matches the oracle."""
+    from ptmi import geom, layout as lay, scenes, shapes
+    w, h, spp = 40, 32, 4
+    sc = scenes.reference_scene(w, h)
+    tiny = shapes.Sphere()
+    tiny.set_transform(geom.translate(0.1, 0.1, -0.2))
+    tiny.set_transform(geom.scale(2.0 ** -70, 2.0 ** -70, 2.0 ** -70))
+    tiny.set_material(shapes.new_diffuse(0.5, 0.5, 0.5))
+    objs, tris, grps = lay.build_scene_buffer_cl(sc.objects + [tiny])
+    cam = lay.camera_record(sc.camera)
+    seeds = layout.seeds_go_float64(w * h, 5)
+    t2, g2 = layout.pad_empty(tris, grps)
+    ora = pyoracle.cpu_trace(objs, t2, g2, cam, spp, seeds)
+    out = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    assert np.abs(out - ora).max() < TOL
+
+
 def test_hip_matches_cpu_oracle_odd_size():
     w, h, spp = 37, 23, 7   # not a multiple of the 8x8 tile
     objs, tris, grps, cam = scene_inputs("default", w, h)
