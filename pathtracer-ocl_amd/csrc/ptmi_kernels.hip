@@ -237,6 +237,14 @@ __device__ __forceinline__ double row1(const double* __restrict__ m, bool st, d4
     return st ? m[5] * v.y + m[7] * v.w : ((m[4] * v.x + m[5] * v.y) + m[6] * v.z) + m[7] * v.w;
 }
 
+// ocml's sin_f32 out of line: only arguments >= 2^19 reach it (sample indices above
+// ~2210, or the n*n of refractive materials), so its general reduction is not inlined
+// into every noise call.
+#ifndef PTMI_SIN_FALLBACK_INLINE
+#define PTMI_SIN_FALLBACK_INLINE __noinline__
+#endif
+__device__ PTMI_SIN_FALLBACK_INLINE float sinf_ocml(float x) { return sinf(x); }
+
 // noise3D (tracer.cl:314-317): float math, ocml sin_f32, ocml fract_f32.
 __device__ __forceinline__ float noise3d(float x, float y, float z) {
     if (PTMI_ABLATE & 1) {
@@ -257,7 +265,7 @@ __device__ __forceinline__ float noise3d(float x, float y, float z) {
     if (fabsf(s) < 0x1p19f) {
         sn = sinf_lt19(s);
     } else {
-        sn = sinf(s);
+        sn = sinf_ocml(s);
     }
     float v = sn * 43758.5453f;
     return fminf(v - floorf(v), 0x1.fffffep-1f);
@@ -1306,7 +1314,8 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
 // Writes the chunk's RGB sums (A = #samples) to out[(chunk*npix + pixel)*4].
 template <int FL>
 #ifndef PTMI_WAVES
-#define PTMI_WAVES 4        // waves/SIMD the register allocation targets (scenes without groups)
+#define PTMI_WAVES 5        // waves/SIMD the register allocation targets (scenes without groups): 96 VGPRs
+                            // with 64 B/lane of spilled loop invariants beat 4 waves without (C2 -1.3 %, C3 -2.9 %)
 #endif
 #ifndef PTMI_WAVES_GROUPS
 #define PTMI_WAVES_GROUPS 3  // ... and with BVH groups (the walk needs more registers; 4 spills)
