@@ -14,6 +14,9 @@
 // result bit in the domain -- checked for every float |x| < 2^19 against the
 // oracle's restatement (tools/sinf_check.cpp) and against the device library
 // itself (tests/test_gpu_rng.py).  Without p4 as well, 38 floats would differ.
+// The reduced argument itself is then F' * pi/2 in FP64 rounded once to float,
+// except within a guard band around float rounding midpoints, where ocml's own
+// truncated hi/lo sequence runs (PTMI_SIN_FP64R; same checks).
 // The small-argument path, the polynomials and the sign logic are ocml's,
 // operation for operation (cf. oracle/ocml_sinf.h, verified against ocml over
 // all 2^32 floats).
@@ -26,6 +29,9 @@
 
 #ifndef PTMI_SINF_FN
 #define PTMI_SINF_FN __device__ __forceinline__
+#endif
+#ifndef PTMI_SIN_FP64R
+#define PTMI_SIN_FP64R 1  // large-argument r from one FP64 product (ocml's hi/lo sequence near midpoints only)
 #endif
 
 namespace ptmi {
@@ -80,6 +86,20 @@ PTMI_SINF_FN float sf_redux_large_17_19(float x, int& q) {
     const uint32_t a73 = 0u - a72;
     const uint32_t a74 = a68 << 31;
     const uint32_t a75 = a69 ^ a73, a76 = a70 ^ a73, a77 = a71 ^ a73;
+    q = (int)((a72 + (a65 >> 30)) & 3u);
+#if PTMI_SIN_FP64R
+    // ocml turns F' = a75:a76:a77 * 2^-96 (< 1/2) into a truncated float pair hi + lo and
+    // returns r = RN(p + e1) = RN(F' pi/2 (1 + d)), |d| < 2^-46.  F' pi/2 in FP64 (relative
+    // error < 2^-51), rounded once to float, is the same r unless it lies within 2^9 double
+    // ulps of a float rounding midpoint (low 29 mantissa bits near 0x10000000): those rare
+    // lanes (24 of the 2^24 floats in [2^18, 2^19)) take ocml's sequence below.
+    {
+        const double fd = fma((double)a76, 0x1p-32, (double)a75) + (double)a77 * 0x1p-64;
+        const double rd = fd * (0x1p-32 * 1.5707963267948966);
+        const uint32_t tail = ((uint32_t)__builtin_bit_cast(uint64_t, rd) + 0x200u) & 0x1FFFFFFFu;
+        if (a75 != 0u && tail - 0x10000000u >= 0x400u) return sf_float(sf_bits((float)rd) ^ a74);
+    }
+#endif
     const uint32_t a78 = sf_clz(a75);
     const uint32_t a79 = 31u - a78;
     const uint32_t a80 = sf_fshr(a75, a76, a79);
@@ -94,7 +114,6 @@ PTMI_SINF_FN float sf_redux_large_17_19(float x, int& q) {
     float e1 = fmaf(hi, pio2_hi, -p);
     e1 = fmaf(hi, pio2_mid, e1);
     e1 = fmaf(lo, pio2_hi, e1);
-    q = (int)((a72 + (a65 >> 30)) & 3u);
     return e1 + p;
 }
 
