@@ -106,6 +106,28 @@ def test_affine_cores_match_generic_large(monkeypatch, scene, ap):
     assert np.array_equal(spec, gen)
 
 
+@pytest.mark.parametrize("scene,w,h,spp,ap,fl,seed", [
+    ("reference", 24, 16, 1300, 0.0, 0.0, 201),
+    ("reference", 16, 16, 1200, 0.15, 1.6, 202),
+    ("teapot", 16, 12, 1100, 0.0, 0.0, 203),
+    ("gopher", 16, 12, 900, 0.0, 0.0, 204),
+])
+def test_hip_matches_live_reference_high_sample_indices(scene, w, h, spp, ap, fl, seed):
+    """Sample indices past ~550 put the noise's sin arguments above 2^17, onto the
+    large-argument reduction (csrc/ptmi_sinf.h); short frames never reach it.  Small
+    images at ~1000 spp against the live reference kernel: any noise bit off moves a
+    pixel by ~1/spp, far above the 1e-12 asserted."""
+    if not pyoracle.ref_available():
+        pytest.skip("oracle/_ref not built")
+    objs, tris, grps, cam = scene_inputs(scene, w, h, ap, fl)
+    seeds = layout.seeds_go_float64(w * h, seed)
+    t2, g2 = layout.pad_empty(tris, grps)
+    ref = pyoracle.ref_trace(objs, t2, g2, cam, spp, seeds)
+    out = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    err = np.abs(out - ref).max()
+    assert err < 1e-12, "%s: L-inf %.3e vs live reference at %d spp" % (scene, err, spp)
+
+
 def test_untame_scene_matches_cpu_oracle():
     """A sphere scaled by 2^-70 (inverse entries 2^70, outside the tame-scene bound of
     ptmi_api.cpp) sends the scene to the generic instantiation with the compiler's full
