@@ -111,6 +111,9 @@ def test_affine_cores_match_generic_large(monkeypatch, scene, ap):
     ("reference", 16, 16, 1200, 0.15, 1.6, 202),
     ("teapot", 16, 12, 1100, 0.0, 0.0, 203),
     ("gopher", 16, 12, 900, 0.0, 0.0, 204),
+    # glass: noise3D(fgi, n*n, b) puts arguments far above 2^19 -> ocml's own sin (out of line)
+    ("transparency", 16, 12, 400, 0.0, 0.0, 205),
+    ("transparent_teapot", 16, 12, 300, 0.0, 0.0, 206),
 ])
 def test_hip_matches_live_reference_high_sample_indices(scene, w, h, spp, ap, fl, seed):
     """Sample indices past ~550 put the noise's sin arguments above 2^17, onto the
