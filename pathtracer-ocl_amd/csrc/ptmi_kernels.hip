@@ -297,8 +297,9 @@ __device__ __forceinline__ bool ray_box(d4 o, d4 d, const double* mn, const doub
 
 struct Hit {
     double t;
-    int obj;    // slot in DevScene::objs (type-run order)
-    int key;    // the object's index in the reference's list
+    int pk;     // (key << 16) | slot: the object's index in the reference's list and its
+                // slot in DevScene::objs (type-run order); -1 = no hit.  One select per
+                // candidate instead of two, and key order is pk order (keys are distinct).
     int tri;    // reference triangle index, -1 for other shapes
     int chain;  // the triangle's gate-chain code (DevTri::chain)
     double u, v;
@@ -311,21 +312,23 @@ struct Hit {
 // the lexicographic minimum (t, key) -- the same candidate.  Candidates of one
 // object are still produced in the reference's order (strict < keeps the first).
 // Evaluated without short-circuits: compares and mask ops, no exec-mask branches.
-__device__ __forceinline__ bool better(const Hit& h, double t, int key) {
-    return (t > kEps) & ((t < h.t) | ((t == h.t) & (key < h.key)));
+__device__ __forceinline__ int pack_hit(int slot, int key) { return (key << 16) | slot; }
+__device__ __forceinline__ int hit_obj(const Hit& h) { return h.pk < 0 ? -1 : (h.pk & 0xFFFF); }
+__device__ __forceinline__ bool better(const Hit& h, double t, int pk) {
+    return (t > kEps) & ((t < h.t) | ((t == h.t) & (pk < h.pk)));
 }
 // Triangles of one group object are recorded by the reference in increasing
 // triangle index (nodes are numbered, and their triangles appended, in the same
 // preorder the walk follows: scene.go:96-155, tracer.cl:621-719), so a tie in
 // (t, object) is broken by the triangle index.
-__device__ __forceinline__ bool better_tri(const Hit& h, double t, int key, int tri) {
-    return t > kEps && (t < h.t || (t == h.t && (key < h.key || (key == h.key && tri < h.tri))));
+__device__ __forceinline__ bool better_tri(const Hit& h, double t, int pk, int tri) {
+    return t > kEps && (t < h.t || (t == h.t && (pk < h.pk || (pk == h.pk && tri < h.tri))));
 }
 __device__ __forceinline__ void consider(Hit& h, double t, int obj, int key) {
-    if (better(h, t, key)) {
+    const int pk = pack_hit(obj, key);
+    if (better(h, t, pk)) {
         h.t = t;
-        h.obj = obj;
-        h.key = key;
+        h.pk = pk;
         h.tri = -1;
     }
 }
@@ -464,7 +467,7 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 
     dt = fma(e2z, qz, dt);
     const double t = f * dt;
     const int n = T.n;
-    if (better_tri(h, t, key, n)) {
+    if (better_tri(h, t, pack_hit(slot, key), n)) {
         const int c = T.chain;
         // Eager mode admits the hit only if the reference would have tested this
         // triangle: its gate chain (root -> its node) passes the exact line-box
@@ -479,8 +482,7 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 
         }
         h.chain = c;
         h.t = t;
-        h.obj = slot;
-        h.key = key;
+        h.pk = pack_hit(slot, key);
         h.tri = n;
         h.u = u;
         h.v = v;
@@ -647,10 +649,10 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
 // Candidate update as selects (no exec-mask branching).  t > EPSILON implies
 // the reference's `t != 0.0` recording test.
 __device__ __forceinline__ void consider_sel(Hit& h, double t, int obj, int key) {
-    const bool c = better(h, t, key);
+    const int pk = pack_hit(obj, key);
+    const bool c = better(h, t, pk);
     h.t = c ? t : h.t;
-    h.obj = c ? obj : h.obj;
-    h.key = c ? key : h.key;
+    h.pk = c ? pk : h.pk;
     h.tri = c ? -1 : h.tri;
 }
 
@@ -701,7 +703,7 @@ __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int ke
 template <int FL>
 __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 rd) {
     constexpr bool A = !(FL & F_PROJ);
-    Hit h{1024.0, -1, -1, -1, -1, 0.0, 0.0};
+    Hit h{1024.0, -1, -1, -1, 0.0, 0.0};
     // Plane and sphere records are scalar loads; the next object's record is loaded
     // while the current one is intersected (its latency is otherwise exposed on
     // every object).  Duplicate-free: the last iteration re-loads its own record.
@@ -724,8 +726,7 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     auto plane_take = [&](const PlaneRec& P, double q, bool ok) {
         const bool c = ok & (q < h.t);
         h.t = c ? q : h.t;
-        h.obj = c ? P.slot : h.obj;
-        h.key = c ? P.key : h.key;
+        h.pk = c ? pack_hit(P.slot, P.key) : h.pk;
     };
     int p = 0;
     for (; p + 1 < np; p += 2) {
@@ -877,7 +878,7 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restr
         }
         // Tentative walks: certify the gate chain of a winner from this object while
         // its object-space ray is at hand (a later object that takes over re-certifies).
-        if (!kVerify && h.tri >= 0 && h.obj == j) cert = chain_certified(S, h.chain, o, d, h.t);
+        if (!kVerify && h.tri >= 0 && hit_obj(h) == j) cert = chain_certified(S, h.chain, o, d, h.t);
     }
 }
 
@@ -897,7 +898,7 @@ __device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__
 #if !(defined(PTMI_EXP) && (PTMI_EXP & 8))
     if (h.tri >= 0) PTMI_COUNT(4);
     if (h.tri >= 0 && !cert) {  // the winner is a triangle (h0 holds primitives only) without certificate
-        const DevObject& ob = S.objs[h.obj];
+        const DevObject& ob = S.objs[hit_obj(h)];
         const d4 o = xpt<A>(ob.inv, ob.st, ro);
         const d4 d = xdir<A>(ob.inv, ob.st, rd);
         if (!verify_chain(S, h.chain, o, d)) {
@@ -1177,8 +1178,8 @@ __device__ __noinline__ d4 plane_normal_map(const DevTexArray T, const DevObject
 template <int FL>
 __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, const Hit& h, float fgi, uint32_t n) {
     constexpr bool A = !(FL & F_PROJ);
-    if (h.obj < 0) return true;  // a miss repeats identically until b == 10 in the reference
-    const DevObject& ob = S.objs[h.obj];
+    if (h.pk < 0) return true;  // a miss repeats identically until b == 10 in the reference
+    const DevObject& ob = S.objs[h.pk & 0xFFFF];
     const int type = ob.type;
     const uint32_t b = P.b;
     d4 pos = add4(P.ro, scl4(P.rd, h.t));
@@ -1438,7 +1439,7 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
 #endif
         if (active && !pending) {
             if (P.dead) {
-                h.obj = -1;
+                h.pk = -1;
                 ready = true;
             } else {
                 h = find_closest_prims<FL>(S, P.ro, P.rd);
