@@ -33,6 +33,9 @@
 #ifndef PTMI_SIN_FP64R
 #define PTMI_SIN_FP64R 1  // large-argument r from one FP64 product (ocml's hi/lo sequence near midpoints only)
 #endif
+#ifndef PTMI_SIN_CW64
+#define PTMI_SIN_CW64 1  // large-argument reduction by FP64 Cody-Waite (Payne-Hanek only near ties)
+#endif
 
 namespace ptmi {
 
@@ -63,6 +66,29 @@ PTMI_SINF_FN float sf_redux_small(float x, int& q) {
 
 // __ocmlpriv_trigredlarge_f32 specialised to 2^17 <= x < 2^19 (exponent 144, 145).
 PTMI_SINF_FN float sf_redux_large_17_19(float x, int& q) {
+#if PTMI_SIN_CW64
+    // ocml's large reduction returns k = the nearest integer to x 2/pi (as q = k mod 4)
+    // and r = RN((x - k pi/2) (1 + d)), |d| < 2^-46.  For x < 2^19 a three-part FP64
+    // Cody-Waite step gives x - k pi/2 to ~2^-51 relative: pi/2 = P1 + P2 + P3 with a
+    // 33-bit P1, so k P1 (k < 2^19) and x - k P1 are exact and the two remaining fmas
+    // round once each.  That r rounded once to float is ocml's r except (a) when x 2/pi
+    // lies so close to a half-integer that the FP64 product may round k the other way
+    // (then |r| is within 2^-25 of pi/4), or (b) within the midpoint guard band of the
+    // FP64R block below; both take the Payne-Hanek path.  Same exhaustive checks.
+    {
+        const double xd = (double)x;
+        const double kd = __builtin_rint(xd * 0x1.45f306dc9c883p-1);
+        double r = fma(-kd, 0x1.921fb54400000p+0, xd);
+        r = fma(-kd, 0x1.0b4611a600000p-34, r);
+        r = fma(-kd, 0x1.3198a2e037073p-69, r);
+        const uint64_t rb = __builtin_bit_cast(uint64_t, r);
+        const uint32_t tail = ((uint32_t)rb + 0x200u) & 0x1FFFFFFFu;
+        if (((uint32_t)(rb >> 32) & 0x7FFFFFFFu) < 0x3FE921FBu && tail - 0x10000000u >= 0x400u) {
+            q = ((int)kd) & 3;
+            return (float)r;
+        }
+    }
+#endif
     const uint32_t bits = sf_bits(x);
     const uint32_t e = bits >> 23;
     const uint64_t m = (uint64_t)((bits & 0x7FFFFFu) | 0x800000u);
