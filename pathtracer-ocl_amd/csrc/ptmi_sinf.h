@@ -17,6 +17,8 @@
 // The reduced argument itself is then F' * pi/2 in FP64 rounded once to float,
 // except within a guard band around float rounding midpoints, where ocml's own
 // truncated hi/lo sequence runs (PTMI_SIN_FP64R; same checks).
+// Ahead of all that, an FP64 Cody-Waite step (PTMI_SIN_CW64) computes the same r and
+// q for all but 28 of the 2^24 floats in [2^17, 2^19); those lanes take the product.
 // The small-argument path, the polynomials and the sign logic are ocml's,
 // operation for operation (cf. oracle/ocml_sinf.h, verified against ocml over
 // all 2^32 floats).
