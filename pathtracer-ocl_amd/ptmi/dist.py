@@ -6,9 +6,10 @@ sample index n, total samples S) (tracer.cl:840-869), so a frame shards with no
 data-path exchange; the only collective is the final sum of the per-rank
 partial framebuffers:
 
-  * sample split -- rank r renders samples [r*S/N, (r+1)*S/N) of every pixel
-    (global n and total S are passed through, so fgi2 = seed/S and the DoF
-    sunflower pattern are those of the full frame);
+  * sample split -- rank r renders a contiguous range of sample indices of every
+    pixel (global n and total S are passed through, so fgi2 = seed/S and the DoF
+    sunflower pattern are those of the full frame).  The ranges are balanced by
+    cost, not count (sample_split_point);
   * tile split   -- rank r renders every sample of the 8x8 tiles t with
     t % N == r (round-robin, balances a mesh-heavy region across ranks) and
     leaves the other pixels at exactly 0.
@@ -21,13 +22,44 @@ differs from a one-GPU render only by FP64 summation order (~1e-16 relative).
 """
 TILE = 8  # ptmi_device.h kTile
 
+# Relative cost of one sample by its index n (x50): past n ~ 553 the hemisphere noise
+# arguments (n * 237.212 + ...) and past ~731 the anti-aliasing ones (n * 179.233)
+# reach 2^17, ocml's large-argument sin reduction (csrc/ptmi_sinf.h).  Measured on
+# C2 (tools/sample_cost.py): 256-sample slices take 23.5 ms below n = 512 and 24.5 ms
+# above 768.  Same table as ptmi_api.cpp's split_point.
+_COST_KNOTS = ((553, 50), (731, 51))
+_COST_TAIL = 52
+
+
+def _cost(n):
+    c, lo = 0, 0
+    for hi, w in _COST_KNOTS:
+        c += w * max(0, min(n, hi) - lo)
+        lo = hi
+    return c + _COST_TAIL * max(0, n - lo)
+
+
+def sample_split_point(g, world, samples):
+    """First sample index of rank g (g = world -> samples): the smallest n whose
+    cumulative cost reaches g/world of the frame's.  Monotone in g, 0 at g = 0."""
+    target = -(-g * _cost(samples) // world)  # ceil
+    n, c, lo = 0, 0, 0
+    for hi, w in _COST_KNOTS + ((1 << 62, _COST_TAIL),):
+        span = w * (hi - lo)
+        if target <= c + span:
+            n = lo + -(-(target - c) // w)
+            break
+        c += span
+        lo = hi
+    return min(n, samples)
+
 
 def shard(rank, world, samples, split):
     """-> (sample_begin, sample_end, tile_stride, tile_offset) of `rank`."""
     if not (0 <= rank < world):
         raise ValueError("rank %d outside world %d" % (rank, world))
     if split == "sample":
-        return rank * samples // world, (rank + 1) * samples // world, 1, 0
+        return sample_split_point(rank, world, samples), sample_split_point(rank + 1, world, samples), 1, 0
     if split == "tile":
         return 0, samples, world, rank
     raise ValueError("split must be 'sample' or 'tile', got %r" % (split,))

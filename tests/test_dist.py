@@ -100,3 +100,17 @@ def test_two_rank_frame_matches_single_process(tmp_path, split):
         rgb = sums[:, :3] * (1.0 / S)  # ptmi_finalize (tracer.cl:1184-1187)
         err = np.abs(rgb - full[:, :3]).max()
         assert err < 1e-12, err  # summation order only
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("samples", [64, 1000, 2048, 4096])
+def test_sample_split_balances_cost(world, samples):
+    """Ranks get equal cost, not equal counts: the late sample indices (large-argument
+    noise sin) weigh more, so the early ranks take a few more samples."""
+    pts = [pdist.sample_split_point(g, world, samples) for g in range(world + 1)]
+    costs = [pdist._cost(b) - pdist._cost(a) for a, b in zip(pts, pts[1:])]
+    per_sample = max(pdist._COST_TAIL, max(w for _, w in pdist._COST_KNOTS))
+    assert max(costs) - min(costs) <= 2 * per_sample
+    if samples > 731 * 2:
+        counts = [b - a for a, b in zip(pts, pts[1:])]
+        assert counts[0] > counts[-1]
