@@ -505,13 +505,14 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     const uint32_t tiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
     const uint32_t owned_tiles = (tiles + tile_stride - 1 - tile_offset) / tile_stride;
     if (chunks == 0) {
-        // ~32 work items (tile x sample chunk) per resident wave slot, >= 64 samples per
+        // ~32 work items (tile x sample chunk) per resident wave slot, >= 32 samples per
         // chunk: short items shorten the end-of-launch tail, while each item pays a fixed
         // start-up.  Measured (one MI355X, 2048 spp): C2 242.7 ms at 2 chunks, 234.5 at 7,
         // 233.3 at 12; teapot 922 / 862 / 885 ms at 2 / 6 / 16; gopher 1484 / 1404 / 1416.
+        // The 256-sample range of one rank of 8: 23.85 / 23.46 / 23.38 ms at 2 / 4 / 8 chunks.
         const uint64_t want = (uint64_t)s->resident_waves * 32;
         chunks = (uint32_t)std::min<uint64_t>((want + owned_tiles - 1) / std::max<uint32_t>(owned_tiles, 1),
-                                              std::max<uint32_t>(range / 64, 1));
+                                              std::max<uint32_t>(range / 32, 1));
     }
     chunks = std::max<uint32_t>(1, std::min<uint32_t>(chunks, std::max<uint32_t>(range, 1)));
     const uint32_t chunk_len = range == 0 ? 1 : (range + chunks - 1) / chunks;
