@@ -85,8 +85,9 @@ int ptmi_trace(const void* objects, uint32_t n_obj, const void* triangles, uint3
  * ptmi_trace_multi -- ptmi_trace over several GPUs of this process:
  * one host thread per entry of devices[0..n_devices) (an index may repeat), each
  * rendering its shard of the frame into its own partial sums:
- *   split 0 (sample): device d renders samples [d*S/n, (d+1)*S/n) of every pixel
- *                     (global sample indices, as ptmi_scene_render);
+ *   split 0 (sample): device d renders a contiguous range of sample indices of
+ *                     every pixel (global indices, as ptmi_scene_render), balanced
+ *                     by cost: late indices weigh ~4 % more (ptmi/dist.py);
  *   split 1 (tile)  : device d renders every sample of the 8x8 tiles t with
  *                     t % n == d.
  * The partial frames are summed on the host in device order (deterministic; the
