@@ -264,7 +264,7 @@ __device__ __forceinline__ float noise3d(float x, float y, float z) {
     float sn;
     if (fabsf(s) < 0x1p19f) {
         sn = sinf_lt19(s);
-    } else {
+    } else if (!(fabsf(s) < 0x1p30f) || !sinf_cw30(s, sn)) {  // glass noise: FP64 Cody-Waite below 2^30
         sn = sinf_ocml(s);
     }
     float v = sn * 43758.5453f;

@@ -170,4 +170,39 @@ PTMI_SINF_FN float sinf_lt19(float x) {
     return sf_float((sf_bits(ax) ^ sf_bits(x)) ^ neg ^ v);
 }
 
+// __ocml_sin_f32 for 2^19 <= |x| < 2^30 (the glass noise, noise3D(fgi, n*n, b)) by a
+// four-part FP64 Cody-Waite reduction: 23-bit P1, P2, P3, so k P1, k P2, k P3 are
+// exact for k < 2^30 and x - k P1, (x - k P1) - k P2 too; the last two fmas round
+// once each (~2^-51 relative).  Returns false, and the caller runs ocml's own sin,
+// where that r may differ from ocml's: k possibly rounded the other way (|r| within
+// 2^-20 of pi/4) or r in the float-midpoint guard band.  Exhaustive host check in
+// tools/sinf_check.cpp.
+PTMI_SINF_FN bool sinf_cw30(float x, float& out) {
+    const float ax = fabsf(x);
+    const double xd = (double)ax;
+    const double kd = __builtin_rint(xd * 0x1.45f306dc9c883p-1);
+    double r = fma(-kd, 0x1.921fb4p+0, xd);
+    r = fma(-kd, 0x1.4442d0p-24, r);
+    r = fma(-kd, 0x1.846988p-48, r);
+    r = fma(-kd, 0x1.8cc51701b839ap-72, r);
+    const uint64_t rb = __builtin_bit_cast(uint64_t, r);
+    const uint32_t tail = ((uint32_t)rb + 0x200u) & 0x1FFFFFFFu;
+    if (!(((uint32_t)(rb >> 32) & 0x7FFFFFFFu) < 0x3FE921F5u && tail - 0x10000000u >= 0x400u)) return false;
+    const int q = ((int)(int64_t)kd) & 3;
+    const float rf = (float)r;
+    const float x2 = rf * rf;
+    float s = fmaf(x2, sf_float(0xB94C1982u), sf_float(0x3C0881C4u));
+    s = fmaf(x2, s, sf_float(0xBE2AAA9Du));
+    s = x2 * s;
+    s = fmaf(rf, s, rf);
+    float c = fmaf(x2, sf_float(0x37D75334u), sf_float(0xBAB64F3Bu));
+    c = fmaf(x2, c, sf_float(0x3D2AABF7u));
+    c = fmaf(x2, c, sf_float(0xBF000004u));
+    c = fmaf(x2, c, 1.0f);
+    const uint32_t v = (q & 1) ? sf_bits(c) : sf_bits(s);
+    const uint32_t neg = (q > 1) ? 0x80000000u : 0u;
+    out = sf_float((sf_bits(ax) ^ sf_bits(x)) ^ neg ^ v);
+    return true;
+}
+
 }  // namespace ptmi

@@ -26,4 +26,16 @@ int main() {
     }
   }
   printf("mismatches %llu first 0x%08x\n", bad, first);
+  // ptmi::sinf_cw30 (2^19 <= |x| < 2^30, the glass noise) where it returns a result
+  unsigned long long bad2 = 0, fb = 0;
+  #pragma omp parallel for reduction(+:bad2, fb) schedule(static)
+  for (long long i = 0x49000000ll; i < 0x4E800000ll; i++) {
+    for (int sg = 0; sg < 2; sg++) {
+      const float x = pto_bits2f((uint32_t)i | (sg ? 0x80000000u : 0u));
+      float a;
+      if (!ptmi::sinf_cw30(x, a)) { fb++; continue; }
+      if (pto_f2bits(a) != pto_f2bits(pto_sinf(x))) bad2++;
+    }
+  }
+  printf("cw30: mismatches %llu fallbacks %llu of %llu\n", bad2, fb, 2ull * (0x4E800000ull - 0x49000000ull));
 }
