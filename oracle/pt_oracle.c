@@ -837,6 +837,11 @@ void pto_spherical_map(double x, double y, double z, double* uv) { spherical_map
 void pto_cube_uv(double x, double y, double z, double* uv) { cube_uv(mk(x, y, z, 1.0), &uv[0], &uv[1]); }
 
 float pto_noise3d(float x, float y, float z) { return noise3d(x, y, z); }
+/* intersectRayWithBox (tracer.cl:270-280) on a ray given as o[4], d[4] and a box mn[3], mx[3]. */
+int pto_ray_box(const double* o, const double* d, const double* mn, const double* mx) {
+    return ray_box(mk(o[0], o[1], o[2], o[3]), mk(d[0], d[1], d[2], d[3]), mk(mn[0], mn[1], mn[2], 1.0),
+                   mk(mx[0], mx[1], mx[2], 1.0));
+}
 
 /* Event totals of the last pto_trace call (PTO_COUNT build; else returns 0). */
 int pto_event_counts(uint64_t* out, int n) {

@@ -89,6 +89,8 @@ def _cpu_lib():
         for f in (_cpu.pto_spherical_map, _cpu.pto_cube_uv):
             f.restype = None
             f.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
+        _cpu.pto_ray_box.restype = ctypes.c_int
+        _cpu.pto_ray_box.argtypes = [ctypes.c_void_p] * 4
         _cpu.pto_noise3d.restype = ctypes.c_float
         _cpu.pto_noise3d.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float]
         _cpu.pto_sinf32.restype = ctypes.c_float
@@ -159,6 +161,12 @@ def cpu_trace(objects, triangles, groups, camera, samples, seeds, row0=0, rows=N
     if rc != 0:
         raise RuntimeError("pto_trace rc=%d" % rc)
     return out
+
+
+def ray_box(origin, direction, bb_min, bb_max):
+    """intersectRayWithBox (tracer.cl:270-280): origin/direction 4-tuples, box corners 3-tuples."""
+    a = [np.ascontiguousarray(v, dtype=np.float64) for v in (origin, direction, bb_min, bb_max)]
+    return bool(_cpu_lib().pto_ray_box(*[x.ctypes.data_as(ctypes.c_void_p) for x in a]))
 
 
 def noise3d(x, y, z):

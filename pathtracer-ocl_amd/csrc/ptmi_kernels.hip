@@ -237,9 +237,10 @@ __device__ __forceinline__ double row1(const double* __restrict__ m, bool st, d4
     return st ? m[5] * v.y + m[7] * v.w : ((m[4] * v.x + m[5] * v.y) + m[6] * v.z) + m[7] * v.w;
 }
 
-// ocml's sin_f32 out of line: only arguments >= 2^19 reach it (sample indices above
-// ~2210, or the n*n of refractive materials), so its general reduction is not inlined
-// into every noise call.
+// ocml's sin_f32 out of line: only noise arguments >= 2^30, and the few lanes of
+// [2^19, 2^30) near a tie or float midpoint that sinf_cw30 declines, reach it
+// (2^19 is passed at sample indices above ~2210, or by the n*n of refractive
+// materials), so its general reduction is not inlined into every noise call.
 #ifndef PTMI_SIN_FALLBACK_INLINE
 #define PTMI_SIN_FALLBACK_INLINE __noinline__
 #endif
@@ -259,14 +260,10 @@ __device__ __forceinline__ float noise3d(float x, float y, float z) {
     // Every call site passes finite floats below 2^33 (fgi, fgi2 in [0, 1], sample and
     // bounce indices and n*n as u32), so s, sin(s) and v are finite and ocml fract's
     // NaN / inf cases (fract(NaN) = NaN, fract(inf) = 0) are unreachable.
-    // ocml's sin_f32, bit for bit; below 2^19 (every bench argument) with the
-    // specialised reduction of ptmi_sinf.h, above it through ocml itself.
-    float sn;
-    if (fabsf(s) < 0x1p19f) {
-        sn = sinf_lt19(s);
-    } else if (!(fabsf(s) < 0x1p30f) || !sinf_cw30(s, sn)) {  // glass noise: FP64 Cody-Waite below 2^30
-        sn = sinf_ocml(s);
-    }
+    // ocml's sin_f32, bit for bit (ptmi_sinf.h noise_sinf): below 2^19 (every bench
+    // argument) the specialised reduction, up to 2^30 (glass noise) an FP64 Cody-Waite
+    // step, else and near ties ocml itself (out of line).
+    const float sn = noise_sinf(s, [](float v) { return sinf_ocml(v); });
     float v = sn * 43758.5453f;
     return fminf(v - floorf(v), 0x1.fffffep-1f);
 }

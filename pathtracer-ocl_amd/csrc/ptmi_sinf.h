@@ -205,4 +205,20 @@ PTMI_SINF_FN bool sinf_cw30(float x, float& out) {
     return true;
 }
 
+// The kernel's noise sin (noise3d in ptmi_kernels.hip), composed in one place so the
+// GPU probe (tests/gpu_probe/sinf_probe.hip) checks exactly what the kernel runs:
+//   |x| < 2^19           sinf_lt19 (every argument of a <= 2210-spp frame but glass)
+//   2^19 <= |x| < 2^30   sinf_cw30, or `fallback` (ocml's own sin) where it declines
+//   otherwise            `fallback`
+template <typename Fallback>
+PTMI_SINF_FN float noise_sinf(float x, Fallback fallback) {
+    float sn;
+    if (fabsf(x) < 0x1p19f) {
+        sn = sinf_lt19(x);
+    } else if (!(fabsf(x) < 0x1p30f) || !sinf_cw30(x, sn)) {
+        sn = fallback(x);
+    }
+    return sn;
+}
+
 }  // namespace ptmi

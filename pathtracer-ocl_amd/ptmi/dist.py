@@ -82,3 +82,21 @@ def reduce_frame(partial, group=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(partial, op=dist.ReduceOp.SUM, group=group)
     return partial
+
+
+def reduce_frame_to(partial, dst=0, group=None, via_host=False):
+    """Sum the ranks' partial framebuffers onto rank `dst` (one RCCL reduce of
+    W*H*4 doubles over xGMI on a GPU node -- SURVEY.md 8e's ncclReduce; only the
+    destination normalises and keeps the frame).  ``via_host``: reduce a host copy
+    (gloo), for ranks that share one device in a rehearsal.  No-op at N=1."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
+        return partial
+    if via_host:
+        h = partial.cpu()
+        dist.reduce(h, dst, op=dist.ReduceOp.SUM, group=group)
+        if dist.get_rank(group) == dst:
+            partial.copy_(h)
+    else:
+        dist.reduce(partial, dst, op=dist.ReduceOp.SUM, group=group)
+    return partial

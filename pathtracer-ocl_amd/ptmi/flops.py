@@ -56,3 +56,15 @@ def flops_per_sample(counts):
     f64 = sum(FP64_COST[e] * counts[e] for e in EVENTS) / n
     f32 = sum(FP32_COST.get(e, 0) * counts[e] for e in EVENTS) / n
     return f64, f32
+
+
+# Algorithmic bytes of the BVH scenes' memory traffic: under the
+# reference's visit rules (tracer.cl:617-719) every node whose box is tested is fetched
+# (64 B: its box + children, compact), every triangle tested fetches p1, e1, e2 (72 B of
+# FP64) and every winning triangle its normals and colour (96 B).
+BYTES = {"node_box": 64, "tri_det": 72, "nrm_tri": 96}
+
+
+def bytes_per_sample(counts):
+    """counts: {event: total} for N samples -> algorithmic HBM bytes per sample."""
+    return sum(b * counts[e] for e, b in BYTES.items()) / counts["sample"]

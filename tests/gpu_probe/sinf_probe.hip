@@ -42,6 +42,28 @@ __global__ void ptmi_sinf_check(uint64_t base, uint64_t count, unsigned long lon
     }
 }
 
+// The kernel's complete noise sin (ptmi_sinf.h noise_sinf: sinf_lt19 below 2^19,
+// sinf_cw30 up to 2^30 with ocml's own sin where it declines, ocml above) against the
+// device library, for every float; fb counts the [2^19, 2^30) lanes cw30 declines.
+__global__ void ptmi_noise_sinf_check(uint64_t base, uint64_t count, unsigned long long* mism, unsigned int* first,
+                                      unsigned long long* fb) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t bits = (uint32_t)(base + i);
+    const float x = pto_bits2f(bits);
+    const float ax = fabsf(x);
+    if (ax >= 0x1p19f && ax < 0x1p30f) {
+        float t;
+        if (!ptmi::sinf_cw30(x, t)) atomicAdd(fb, 1ull);
+    }
+    const float a = sinf(x);
+    const float b = ptmi::noise_sinf(x, [](float v) { return sinf(v); });
+    if (pto_f2bits(a) != pto_f2bits(b) && !(a != a && b != b)) {
+        atomicAdd(mism, 1ull);
+        atomicMin(first, bits);
+    }
+}
+
 // Random doubles with a uniform exponent in [emin, emax], random mantissa and sign.
 __device__ static inline uint64_t splitmix(uint64_t& z) {
     z += 0x9E3779B97F4A7C15ull;
@@ -176,5 +198,29 @@ extern "C" int probe_sinf_eval(const float* in, float* out, uint64_t n) {
     (void)hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost);
     (void)hipFree(din);
     (void)hipFree(dout);
+    return 0;
+}
+
+extern "C" int probe_ptmi_noise_sinf_all(unsigned long long* mismatches, unsigned int* first_bad,
+                                         unsigned long long* cw30_fallbacks) {
+    unsigned long long *dm, *dfb;
+    unsigned int* df;
+    if (hipMalloc(&dm, 8) || hipMalloc(&df, 4) || hipMalloc(&dfb, 8)) return -1;
+    (void)hipMemset(dm, 0, 8);
+    (void)hipMemset(dfb, 0, 8);
+    (void)hipMemset(df, 0xff, 4);
+    const uint64_t chunk = 1ull << 28;
+    for (uint64_t base = 0; base < (1ull << 32); base += chunk) {
+        hipLaunchKernelGGL(ptmi_noise_sinf_check, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, chunk, dm, df,
+                           dfb);
+        if (hipGetLastError() != hipSuccess) return -2;
+    }
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    (void)hipMemcpy(mismatches, dm, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(first_bad, df, 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(cw30_fallbacks, dfb, 8, hipMemcpyDeviceToHost);
+    (void)hipFree(dm);
+    (void)hipFree(df);
+    (void)hipFree(dfb);
     return 0;
 }

@@ -75,7 +75,10 @@ def _worker(rank, world, port, split, out_dir):
         if split == "tile":  # this rank's pixels only, the others exactly 0
             part = part.reshape(H, W, 4) * pdist.tile_owner_mask(W, H, ts, to)[..., None]
         sums = torch.from_numpy(np.ascontiguousarray(part).ravel())
-        pdist.reduce_frame(sums)
+        if split == "sample":
+            pdist.reduce_frame(sums)  # all-reduce
+        else:
+            pdist.reduce_frame_to(sums, 0)  # reduce onto rank 0 (bench.py)
         if rank == 0:
             np.save(os.path.join(out_dir, "frame.npy"), sums.numpy())
     finally:
@@ -114,3 +117,43 @@ def test_sample_split_balances_cost(world, samples):
     if samples > 731 * 2:
         counts = [b - a for a, b in zip(pts, pts[1:])]
         assert counts[0] > counts[-1]
+
+
+_RANK_SCRIPT = """
+import os, sys, json
+import torch, torch.distributed as dist
+dist.init_process_group("gloo")
+r, w = dist.get_rank(), dist.get_world_size()
+assert int(os.environ["LOCAL_RANK"]) == r and os.environ["MASTER_ADDR"] == "127.0.0.1"
+t = torch.tensor([float(r + 1)])
+dist.all_reduce(t)
+with open(os.path.join(sys.argv[1], "rank%d.json" % r), "w") as f:
+    json.dump({"rank": r, "world": w, "sum": t.item()}, f)
+dist.destroy_process_group()
+sys.exit(int(sys.argv[2]) if r == 1 else 0)
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launches_its_own_ranks(tmp_path, world):
+    """bench.py --gpus N without a torch.distributed environment starts N ranks
+    itself (RANK = LOCAL_RANK = 0..N-1, WORLD_SIZE = N, 127.0.0.1 rendezvous) and
+    returns a failing rank's status."""
+    import json
+    import bench
+    script = tmp_path / "rank.py"
+    script.write_text(_RANK_SCRIPT)
+    assert bench.launch_ranks(world, [str(tmp_path), "0"], script=str(script)) == 0
+    got = [json.load(open(tmp_path / ("rank%d.json" % r))) for r in range(world)]
+    assert [g["rank"] for g in got] == list(range(world))
+    assert all(g["world"] == world and g["sum"] == world * (world + 1) / 2 for g in got)
+    assert bench.launch_ranks(world, [str(tmp_path), "3"], script=str(script)) == 3
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "..", "bench.py"), "--gpus", "4"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr

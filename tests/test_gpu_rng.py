@@ -23,6 +23,8 @@ def _lib():
     lib.probe_ptmi_sinf_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
     lib.probe_fp64core.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_ulonglong)]
     lib.probe_sincos_core_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
+    lib.probe_ptmi_noise_sinf_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint),
+                                              ctypes.POINTER(ctypes.c_ulonglong)]
     lib.probe_sinf_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     return lib
 
@@ -42,6 +44,21 @@ def test_kernel_sinf_bit_identical_below_2p19():
     m, f = ctypes.c_ulonglong(), ctypes.c_uint()
     assert lib.probe_ptmi_sinf_all(ctypes.byref(m), ctypes.byref(f)) == 0
     assert m.value == 0, "%d mismatches, first input bits 0x%08x" % (m.value, f.value)
+
+
+def test_kernel_noise_sinf_bit_identical_all_floats():
+    """The kernel's whole noise sin as noise3d composes it (ptmi_sinf.h noise_sinf):
+    sinf_lt19 below 2^19, the four-part FP64 Cody-Waite sinf_cw30 on [2^19, 2^30)
+    (the glass noise's n*n arguments, and every noise past sample ~2210) with ocml's
+    own sin on the lanes it declines, ocml above -- equal to the device library for
+    every one of the 2^32 floats.  The number of declined lanes equals the exhaustive
+    host check's (tools/sinf_check.cpp: 1054 of the 1.8e8 floats, both signs)."""
+    lib = _lib()
+    m, f, fb = ctypes.c_ulonglong(), ctypes.c_uint(), ctypes.c_ulonglong()
+    assert lib.probe_ptmi_noise_sinf_all(ctypes.byref(m), ctypes.byref(f), ctypes.byref(fb)) == 0
+    assert m.value == 0, "%d mismatches, first input bits 0x%08x" % (m.value, f.value)
+    n_range = 2 * (0x4E800000 - 0x49000000)  # floats with 2^19 <= |x| < 2^30, both signs
+    assert fb.value == 1054, "cw30 declined %d of %d lanes (host check: 1054)" % (fb.value, n_range)
 
 
 def test_fp64_cores_match_compiler_operators():

@@ -34,7 +34,7 @@ def main(rows=24, spp_sample=8):
     vp, u32 = ctypes.c_void_p, ctypes.c_uint32
     lib.pto_trace.argtypes = [vp, u32, vp, u32, vp, u32, vp, u32, vp, u32, u32, u32, u32, ctypes.c_int, vp]
     lib.pto_event_counts.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-    out = {"model": "ptmi/flops.py", "sample": "rows every H/%d, %d spp of the frame's sample range" % (rows, spp_sample),
+    out = {"model": "ptmi/flops.py", "bytes_model": "ptmi/flops.py BYTES (reference visit rules)", "sample": "rows every H/%d, %d spp of the frame's sample range" % (rows, spp_sample),
            "workloads": {}}
     for name, (scene, w, h, spp, ap, fl) in WORKLOADS.items():
         objs, tris, grps, cam = scene_inputs(scene, w, h, ap, fl)
@@ -60,6 +60,7 @@ def main(rows=24, spp_sample=8):
         out["workloads"][name] = {"scene": scene, "width": w, "height": h, "samples": spp, "aperture": ap,
                                   "focal_length": fl, "events": counts, "fp64_flops_per_sample": f64,
                                   "fp32_flops_per_sample": f32,
+                                  "bytes_per_sample": flops.bytes_per_sample(counts),
                                   "bounces_per_sample": counts["hit"] / counts["sample"],
                                   "obj_tests_per_sample": counts["obj_test"] / counts["sample"]}
         print("%-28s %7.1f s  fp64 flops/sample %8.1f  hits/sample %.3f  tri tests/sample %.1f" % (
