@@ -104,7 +104,7 @@ Box bounds_of(const Shape* s) {  // BoundsOf (boundingbox.go:96-116)
 }
 
 // SplitBounds (bvh.go:8-44)
-static void split_bounds(const Box& b, Box& left, Box& right) {
+void split_bounds(const Box& b, Box& left, Box& right) {
     const double dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
     double greatest = dx;  // shapes.max (basic.go): strict '>' scan
     if (dy > greatest) greatest = dy;
@@ -134,7 +134,7 @@ static bool contains_point(const Box& b, const Tup& p) {
 static bool contains_box(const Box& b, const Box& c) { return contains_point(b, c.mn) && contains_point(b, c.mx); }
 
 // PartitionChildren (bvh.go:46-70)
-static void partition_children(Arena& A, Shape* g, Shape*& left, Shape*& right) {
+void partition_children(Arena& A, Shape* g, Shape*& left, Shape*& right) {
     left = A.group();
     right = A.group();
     Box lb, rb;
@@ -158,7 +158,7 @@ static void partition_children(Arena& A, Shape* g, Shape*& left, Shape*& right) 
 }
 
 // MakeSubGroup (bvh.go:74-84)
-static void make_sub_group(Arena& A, Shape* g, const std::vector<Shape*>& v) {
+void make_sub_group(Arena& A, Shape* g, const std::vector<Shape*>& v) {
     A.subgroup_counter++;
     Shape* sg = A.group();
     sg->material = g->material;
@@ -296,7 +296,10 @@ ObjModel parse_obj(Arena& A, const std::string& data, const std::string& base_di
     std::istringstream is(data);
     std::string row;
     while (std::getline(is, row)) {
-        if (trim(row).empty()) continue;
+        if (trim(row).empty()) {
+            out.ignored_lines++;
+            continue;
+        }
         const auto p = fields(row);
         const std::string& k = p[0];
         if (k == "mtllib") {
@@ -331,8 +334,12 @@ ObjModel parse_obj(Arena& A, const std::string& data, const std::string& base_di
         } else if (k == "g" || k == "o") {
             current = p.at(1);
             get_group(current);
+        } else {
+            out.ignored_lines++;
         }
     }
+    // strings.Split(data, "\n") also yields the empty row after a final newline
+    if (data.empty() || data.back() == '\n') out.ignored_lines++;
     return out;
 }
 

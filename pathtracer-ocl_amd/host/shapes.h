@@ -97,6 +97,11 @@ struct Arena {
 Box bounds_of(const Shape* s);
 Box parent_space_bounds(const Shape* s);
 void divide(Arena& A, Shape* s, size_t threshold);
+// Divide's steps (bvh.go:8-84), exported for the reference's own known-answer tests
+// (tests/host_kat/host_kat.cpp).
+void split_bounds(const Box& b, Box& left, Box& right);
+void partition_children(Arena& A, Shape* g, Shape*& left, Shape*& right);
+void make_sub_group(Arena& A, Shape* g, const std::vector<Shape*>& v);
 
 // OBJ model (obj/objparser.go): groups attached to the root in FILE order (the
 // Go code iterates a map, objparser.go:208-214); mtllib resolved next to the OBJ.
@@ -104,6 +109,7 @@ struct ObjModel {
     std::vector<Tup> vertices{point(0, 0, 0)};
     std::vector<Tup> normals{vector(0, 0, 0)};
     std::vector<std::pair<std::string, Shape*>> groups;
+    size_t ignored_lines = 0;  // Obj.IgnoredLines: blank rows and unknown keywords
     Shape* to_group(Arena& A) const;
 };
 ObjModel parse_obj(Arena& A, const std::string& data, const std::string& base_dir);
