@@ -90,16 +90,39 @@ int ptmi_trace(const void* objects, uint32_t n_obj, const void* triangles, uint3
  *                     by cost: late indices weigh ~4 % more (ptmi/dist.py);
  *   split 1 (tile)  : device d renders every sample of the 8x8 tiles t with
  *                     t % n == d.
- * The partial frames are summed on the host in device order (deterministic; the
- * tile split is exact, the sample split differs from one device only by FP64
- * summation order) and normalised as ptmi_finalize.  Same record / seed / error
- * contract as ptmi_trace.  (The torch.distributed driver, bench.py, does the same
- * with one process per GPU and an RCCL all-reduce.)
+ * The host converts the scene and builds its traversal index once; each device
+ * uploads it.  The partial frames are combined on the device side: peer copies
+ * over xGMI into a gather buffer on devices[0], summed there in device order
+ * (deterministic; the tile split is exact, the sample split differs from one
+ * device only by FP64 summation order) and normalised as ptmi_finalize, then read
+ * back once.  Same record / seed / error contract as ptmi_trace.  (The
+ * torch.distributed driver, bench.py, does the same with one process per GPU and
+ * an RCCL reduce.)
  */
 int ptmi_trace_multi(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
                      const void* groups, uint32_t n_grp, const int* devices, uint32_t n_devices, int split,
                      uint32_t samples, const void* camera, const double* seeds, uint64_t seed_stream,
                      const ptmi_textures* textures, double* out_rgba, char* err, size_t err_len);
+
+/* Wall-clock phases of one ptmi_trace_multi call (milliseconds). */
+typedef struct ptmi_multi_timing {
+    double prepare_ms;  /* host: record conversion + traversal-index build, once for all devices */
+    double render_ms;   /* until the slowest device has its partial frame: upload, seeds, kernels */
+    double combine_ms;  /* from then: xGMI peer copies into the first device + the ordered sum */
+    double readback_ms; /* the RGBA frame to host memory */
+    double total_ms;
+} ptmi_multi_timing;
+
+/* ptmi_trace_multi, also reporting its phases in *timing (may be NULL). */
+int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
+                           const void* groups, uint32_t n_grp, const int* devices, uint32_t n_devices, int split,
+                           uint32_t samples, const void* camera, const double* seeds, uint64_t seed_stream,
+                           const ptmi_textures* textures, double* out_rgba, ptmi_multi_timing* timing, char* err,
+                           size_t err_len);
+
+/* First sample index of device g of n in ptmi_trace_multi's cost-balanced sample
+ * split (g = n -> samples); the same table as bench.py's ranks (ptmi/dist.py). */
+uint32_t ptmi_sample_split_point(int g, int n, uint32_t samples);
 
 /* --list-devices (cmd/pt/main.go:98-112). */
 int ptmi_device_count(void);

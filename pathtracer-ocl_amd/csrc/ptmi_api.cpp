@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdarg>
@@ -29,6 +30,8 @@ hipError_t launch_reduce(const double* part, double* sums, uint32_t npix, uint32
 hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint32_t samples, hipStream_t st);
 hipError_t launch_seeds(double* seeds, uint32_t n, uint64_t stream, hipStream_t st);
 hipError_t launch_plane_normals(DevObject* objs, int n, hipStream_t st);
+hipError_t launch_combine(const double* parts, uint32_t nparts, size_t npix, double* out, uint32_t samples,
+                          hipStream_t st);
 const void* trace_kernel_symbol(int flags);
 int trace_block_threads(int flags);
 }  // namespace ptmi
@@ -254,6 +257,201 @@ int upload(const std::vector<T>& v, void** dst, char* err, size_t err_len) {
     return PTMI_OK;
 }
 
+
+// A scene converted on the host once (records validated and split into the device
+// layouts, traversal indices built, kernel flags chosen), uploadable to any device.
+struct HostScene {
+    std::vector<DevObject> objs;
+    std::vector<int32_t> roots;
+    std::vector<DevNode> nodes;
+    RootIndex index;
+    std::vector<RootRec> root_rec;
+    std::vector<DevTriShade> st;
+    std::vector<PlaneRec> planes;
+    std::vector<SphereRec> spheres;
+    DevCamera cam{};
+    int32_t run_end[5] = {};
+    int flags = 0;
+    uint32_t n_list = 0, n_grp = 0, n_tri = 0;
+};
+
+int prepare_scene(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri, const void* groups,
+                  uint32_t n_grp, const void* camera, const ptmi_textures* textures, HostScene& hs, char* err,
+                  size_t err_len) {
+    int rc = convert_scene((const uint8_t*)objects, n_obj, (const uint8_t*)triangles, n_tri, (const uint8_t*)groups,
+                           n_grp, (const uint8_t*)camera, hs.objs, hs.roots, hs.nodes, hs.index, hs.root_rec, hs.st,
+                           hs.cam, hs.run_end, err, err_len);
+    if (rc) return rc;
+    const DevCamera& cam = hs.cam;
+    int flags = 0;
+    for (const DevObject& o : hs.objs) {
+        if (o.type == 4) flags |= 1;                                    // F_GROUPS
+        if (o.type == 2 || o.type == 3) flags |= 2;                     // F_CYLCUBE
+        if (o.reflectivity != 0.0 || o.refractive_index != 1.0) flags |= 4;  // F_MATERIALS
+    }
+    if (cam.aperture != 0) flags |= 8;                                  // F_DOF
+    // Affine scene (ptmi_kernels.hip dotv): every inverse ends in (+-0, +-0, +-0, 1),
+    // inverse transposes have +-0 in column 3 of rows 0-2, triangle normals have a
+    // finite w.  Otherwise F_PROJ: the generic instantiation with the w lanes.
+    bool affine = cam.inv[12] == 0.0 && cam.inv[13] == 0.0 && cam.inv[14] == 0.0 && cam.inv[15] == 1.0;
+    for (const DevObject& o : hs.objs)
+        affine = affine && o.inv[12] == 0.0 && o.inv[13] == 0.0 && o.inv[14] == 0.0 && o.inv[15] == 1.0 &&
+                 o.inv_t[3] == 0.0 && o.inv_t[7] == 0.0 && o.inv_t[11] == 0.0;
+    for (const DevTriShade& t : hs.st)
+        affine = affine && std::isfinite(t.n1[3]) && std::isfinite(t.n2[3]) && std::isfinite(t.n3[3]);
+    // The affine instantiations also use the compiler's divide / sqrt cores for sphere
+    // roots (ptmi_kernels.hip div_core, DESIGN.md s2 item 8), which needs 2a = 2|M d|^2
+    // far above the denormal range for every unit-scale ray direction d: each sphere's
+    // inverse has linear-part entries <= 2^64 and |det| >= 2^-64, so its smallest singular
+    // value is >= 2^-196.  Scenes outside that take the generic instantiation.
+    // The same bound on the camera inverse keeps |pixel - origin| >= 2^-196 for its
+    // normalize's core, and on sphere inverses (through their transposes) keeps sphere
+    // normals >= 2^-196 long.
+    auto tame = [](const double* m) {
+        double mx = 0.0;
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) mx = std::max(mx, std::fabs(m[4 * r + c]));
+        const double det = m[0] * (m[5] * m[10] - m[6] * m[9]) - m[1] * (m[4] * m[10] - m[6] * m[8]) +
+                           m[2] * (m[4] * m[9] - m[5] * m[8]);
+        return mx <= 0x1p64 && std::fabs(det) >= 0x1p-64;
+    };
+    affine = affine && tame(cam.inv);
+    for (const DevObject& o : hs.objs)
+        if (o.type == 1) affine = affine && tame(o.inv);
+    if (!affine) flags |= 16;                                           // F_PROJ
+    // Textured plane/sphere/cube colours or plane normal maps: the one textured
+    // instantiation (generic arithmetic + software sampler, tracer.cl:907-914, 1077-1092).
+    for (const DevObject& o : hs.objs)
+        if ((o.tex && (o.type == 0 || o.type == 1 || o.type == 3)) || (o.tex_nm && o.type == 0)) flags = 63;
+    if (const char* f = getenv("PTMI_FORCE_FLAGS")) flags = atoi(f) & 63;  // testing: force the generic path
+    if (textures) {
+        for (int k = 0; k < 3; k++) {
+            const uint64_t texels = (uint64_t)textures->width[k] * textures->height[k] * textures->count[k];
+            if (textures->count[k] &&
+                (!textures->pixels[k] || textures->width[k] == 0 || textures->height[k] == 0 ||
+                 textures->width[k] > (1u << 16) || textures->height[k] > (1u << 16) || textures->count[k] > 256 ||
+                 texels > ((uint64_t)1 << 32))) {
+                set_err(err, err_len, "texture array %d: bad size %ux%u x %u layers (or NULL pixels)", k,
+                        textures->width[k], textures->height[k], textures->count[k]);
+                return PTMI_ERR_ARG;
+            }
+        }
+    }
+    hs.flags = flags;
+    // compact plane / scale+translate sphere records (ptmi_device.h)
+    for (size_t k = 0; k < hs.objs.size(); k++) {
+        const DevObject& o = hs.objs[k];
+        if (o.type == 0) {
+            PlaneRec r{};
+            std::memcpy(r.row1, o.inv + 4, 32);
+            r.slot = (int32_t)k;
+            r.key = o.key;
+            hs.planes.push_back(r);
+        } else if (o.type == 1 && o.st) {
+            SphereRec r{};
+            r.m0 = o.inv[0];
+            r.m3 = o.inv[3];
+            r.m5 = o.inv[5];
+            r.m7 = o.inv[7];
+            r.m10 = o.inv[10];
+            r.m11 = o.inv[11];
+            r.m15 = o.inv[15];
+            r.slot = (int32_t)k;
+            r.key = o.key;
+            hs.spheres.push_back(r);
+        }
+    }
+    hs.n_list = n_obj;
+    hs.n_grp = n_grp;
+    hs.n_tri = n_tri;
+    return PTMI_OK;
+}
+
+int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* textures, ptmi_scene** out, char* err,
+                 size_t err_len) {
+    HIP_TRY(hipSetDevice(device_index));
+    ptmi_scene* s = new ptmi_scene();
+    s->flags = hs.flags;
+    s->device = device_index;
+    s->width = (uint32_t)hs.cam.width;
+    s->height = (uint32_t)hs.cam.height;
+    int rc;
+    if ((rc = upload(hs.objs, &s->buffers[0], err, err_len)) || (rc = upload(hs.roots, &s->buffers[1], err, err_len)) ||
+        (rc = upload(hs.nodes, &s->buffers[2], err, err_len)) ||
+        (rc = upload(hs.index.tris, &s->buffers[3], err, err_len)) || (rc = upload(hs.st, &s->buffers[4], err, err_len)) ||
+        (rc = upload(hs.planes, &s->buffers[5], err, err_len)) ||
+        (rc = upload(hs.spheres, &s->buffers[6], err, err_len)) ||
+        (rc = upload(hs.index.nodes, &s->buffers[7], err, err_len)) ||
+        (rc = upload(hs.index.chain_boxes, &s->buffers[8], err, err_len)) ||
+        (rc = upload(hs.root_rec, &s->buffers[9], err, err_len))) {
+        ptmi_scene_destroy(s);
+        return rc;
+    }
+    for (int k = 0; k < 3; k++) {  // texture arrays (prepareTextures, ocltracer.go:228-254)
+        DevTexArray& T = s->dev.tex[k];
+        T = DevTexArray{};
+        if (!textures || textures->count[k] == 0) continue;  // the all-zero fake image
+        const size_t bytes = (size_t)textures->width[k] * textures->height[k] * textures->count[k] * 4;
+        hipError_t e = hipMalloc(&s->buffers[10 + k], bytes);
+        if (e == hipSuccess) e = hipMemcpy(s->buffers[10 + k], textures->pixels[k], bytes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            set_err(err, err_len, "texture array %d upload (%zu B): %s", k, bytes, hipGetErrorString(e));
+            ptmi_scene_destroy(s);
+            return PTMI_ERR_HIP;
+        }
+        T.texels = (const uint32_t*)s->buffers[10 + k];
+        T.w = (int32_t)textures->width[k];
+        T.h = (int32_t)textures->height[k];
+        T.layers = (int32_t)textures->count[k];
+    }
+    s->dev.objs = (const DevObject*)s->buffers[0];
+    for (int t = 0; t < 5; t++) s->dev.run_end[t] = hs.run_end[t];
+    s->dev.planes = (const PlaneRec*)s->buffers[5];
+    s->dev.n_planes = (int32_t)hs.planes.size();
+    s->dev.spheres = (const SphereRec*)s->buffers[6];
+    s->dev.n_spheres_st = (int32_t)hs.spheres.size();
+    // HIP failures from here on release the half-built scene.
+#define SCENE_TRY(call)                                                                            \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            set_err(err, err_len, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
+                    __LINE__);                                                                     \
+            ptmi_scene_destroy(s);                                                                 \
+            return PTMI_ERR_HIP;                                                                   \
+        }                                                                                          \
+    } while (0)
+    if (!hs.objs.empty()) {
+        SCENE_TRY(launch_plane_normals((DevObject*)s->buffers[0], (int)hs.objs.size(), nullptr));
+        SCENE_TRY(hipDeviceSynchronize());
+    }
+    s->dev.roots = (const int32_t*)s->buffers[1];
+    s->dev.nodes = (const DevNode*)s->buffers[2];
+    s->dev.tris = (const DevTri*)s->buffers[3];
+    s->dev.tri_shade = (const DevTriShade*)s->buffers[4];
+    s->dev.nodes4 = (const Node4*)s->buffers[7];
+    s->dev.chains = (const ChainBox*)s->buffers[8];
+    s->dev.root_rec = (const RootRec*)s->buffers[9];
+    s->dev.n_obj = (uint32_t)hs.objs.size();
+    s->dev.n_list = hs.n_list;
+    s->dev.n_nodes = hs.n_grp;
+    s->dev.n_nodes4 = (int32_t)hs.index.nodes.size();
+    s->dev.n_tri = hs.n_tri;
+    s->dev.cam = hs.cam;
+    hipDeviceProp_t p;
+    SCENE_TRY(hipGetDeviceProperties(&p, device_index));
+    s->resident_waves = p.multiProcessorCount * 16;  // refined below from the occupancy query
+    int blocks_per_cu = 0;
+    const int block = trace_block_threads(s->flags);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, trace_kernel_symbol(s->flags), block, 0) ==
+            hipSuccess &&
+        blocks_per_cu > 0)
+        s->resident_waves = p.multiProcessorCount * blocks_per_cu * (block / 64);
+#undef SCENE_TRY
+    *out = s;
+    return PTMI_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -293,178 +491,10 @@ int ptmi_scene_create_textured(int device_index, const void* objects, uint32_t n
     if (device_index < 0) device_index = 0;  // ocltracer.go:138-140
     int rc = check_device(device_index, err, err_len);
     if (rc) return rc;
-    std::vector<DevObject> objs;
-    std::vector<int32_t> roots;
-    std::vector<DevNode> nodes;
-    RootIndex index;
-    std::vector<RootRec> root_rec;
-    std::vector<DevTriShade> st;
-    DevCamera cam{};
-    int32_t run_end[5];
-    rc = convert_scene((const uint8_t*)objects, n_obj, (const uint8_t*)triangles, n_tri, (const uint8_t*)groups, n_grp,
-                       (const uint8_t*)camera, objs, roots, nodes, index, root_rec, st, cam, run_end, err, err_len);
-    if (rc) return rc;
-    int flags = 0;
-    for (const DevObject& o : objs) {
-        if (o.type == 4) flags |= 1;                                    // F_GROUPS
-        if (o.type == 2 || o.type == 3) flags |= 2;                     // F_CYLCUBE
-        if (o.reflectivity != 0.0 || o.refractive_index != 1.0) flags |= 4;  // F_MATERIALS
-    }
-    if (cam.aperture != 0) flags |= 8;                                  // F_DOF
-    // Affine scene (ptmi_kernels.hip dotv): every inverse ends in (+-0, +-0, +-0, 1),
-    // inverse transposes have +-0 in column 3 of rows 0-2, triangle normals have a
-    // finite w.  Otherwise F_PROJ: the generic instantiation with the w lanes.
-    bool affine = cam.inv[12] == 0.0 && cam.inv[13] == 0.0 && cam.inv[14] == 0.0 && cam.inv[15] == 1.0;
-    for (const DevObject& o : objs)
-        affine = affine && o.inv[12] == 0.0 && o.inv[13] == 0.0 && o.inv[14] == 0.0 && o.inv[15] == 1.0 &&
-                 o.inv_t[3] == 0.0 && o.inv_t[7] == 0.0 && o.inv_t[11] == 0.0;
-    for (const DevTriShade& t : st)
-        affine = affine && std::isfinite(t.n1[3]) && std::isfinite(t.n2[3]) && std::isfinite(t.n3[3]);
-    // The affine instantiations also use the compiler's divide / sqrt cores for sphere
-    // roots (ptmi_kernels.hip div_core, DESIGN.md s2 item 8), which needs 2a = 2|M d|^2
-    // far above the denormal range for every unit-scale ray direction d: each sphere's
-    // inverse has linear-part entries <= 2^64 and |det| >= 2^-64, so its smallest singular
-    // value is >= 2^-196.  Scenes outside that take the generic instantiation.
-    // The same bound on the camera inverse keeps |pixel - origin| >= 2^-196 for its
-    // normalize's core, and on sphere inverses (through their transposes) keeps sphere
-    // normals >= 2^-196 long.
-    auto tame = [](const double* m) {
-        double mx = 0.0;
-        for (int r = 0; r < 3; r++)
-            for (int c = 0; c < 3; c++) mx = std::max(mx, std::fabs(m[4 * r + c]));
-        const double det = m[0] * (m[5] * m[10] - m[6] * m[9]) - m[1] * (m[4] * m[10] - m[6] * m[8]) +
-                           m[2] * (m[4] * m[9] - m[5] * m[8]);
-        return mx <= 0x1p64 && std::fabs(det) >= 0x1p-64;
-    };
-    affine = affine && tame(cam.inv);
-    for (const DevObject& o : objs)
-        if (o.type == 1) affine = affine && tame(o.inv);
-    if (!affine) flags |= 16;                                           // F_PROJ
-    // Textured plane/sphere/cube colours or plane normal maps: the one textured
-    // instantiation (generic arithmetic + software sampler, tracer.cl:907-914, 1077-1092).
-    for (const DevObject& o : objs)
-        if ((o.tex && (o.type == 0 || o.type == 1 || o.type == 3)) || (o.tex_nm && o.type == 0)) flags = 63;
-    if (const char* f = getenv("PTMI_FORCE_FLAGS")) flags = atoi(f) & 63;  // testing: force the generic path
-    if (textures) {
-        for (int k = 0; k < 3; k++) {
-            const uint64_t texels = (uint64_t)textures->width[k] * textures->height[k] * textures->count[k];
-            if (textures->count[k] &&
-                (!textures->pixels[k] || textures->width[k] == 0 || textures->height[k] == 0 ||
-                 textures->width[k] > (1u << 16) || textures->height[k] > (1u << 16) || textures->count[k] > 256 ||
-                 texels > ((uint64_t)1 << 32))) {
-                set_err(err, err_len, "texture array %d: bad size %ux%u x %u layers (or NULL pixels)", k,
-                        textures->width[k], textures->height[k], textures->count[k]);
-                return PTMI_ERR_ARG;
-            }
-        }
-    }
-    HIP_TRY(hipSetDevice(device_index));
-    ptmi_scene* s = new ptmi_scene();
-    s->flags = flags;
-    s->device = device_index;
-    s->width = (uint32_t)cam.width;
-    s->height = (uint32_t)cam.height;
-    if ((rc = upload(objs, &s->buffers[0], err, err_len)) || (rc = upload(roots, &s->buffers[1], err, err_len)) ||
-        (rc = upload(nodes, &s->buffers[2], err, err_len)) || (rc = upload(index.tris, &s->buffers[3], err, err_len)) ||
-        (rc = upload(st, &s->buffers[4], err, err_len)) || (rc = upload(index.nodes, &s->buffers[7], err, err_len)) ||
-        (rc = upload(index.chain_boxes, &s->buffers[8], err, err_len)) ||
-        (rc = upload(root_rec, &s->buffers[9], err, err_len))) {
-        ptmi_scene_destroy(s);
+    HostScene hs;
+    if ((rc = prepare_scene(objects, n_obj, triangles, n_tri, groups, n_grp, camera, textures, hs, err, err_len)))
         return rc;
-    }
-    for (int k = 0; k < 3; k++) {  // texture arrays (prepareTextures, ocltracer.go:228-254)
-        DevTexArray& T = s->dev.tex[k];
-        T = DevTexArray{};
-        if (!textures || textures->count[k] == 0) continue;  // the all-zero fake image
-        const size_t bytes = (size_t)textures->width[k] * textures->height[k] * textures->count[k] * 4;
-        hipError_t e = hipMalloc(&s->buffers[10 + k], bytes);
-        if (e == hipSuccess) e = hipMemcpy(s->buffers[10 + k], textures->pixels[k], bytes, hipMemcpyHostToDevice);
-        if (e != hipSuccess) {
-            set_err(err, err_len, "texture array %d upload (%zu B): %s", k, bytes, hipGetErrorString(e));
-            ptmi_scene_destroy(s);
-            return PTMI_ERR_HIP;
-        }
-        T.texels = (const uint32_t*)s->buffers[10 + k];
-        T.w = (int32_t)textures->width[k];
-        T.h = (int32_t)textures->height[k];
-        T.layers = (int32_t)textures->count[k];
-    }
-    s->dev.objs = (const DevObject*)s->buffers[0];
-    for (int t = 0; t < 5; t++) s->dev.run_end[t] = run_end[t];
-    {  // compact plane / scale+translate sphere records (ptmi_device.h)
-        std::vector<PlaneRec> pl;
-        std::vector<SphereRec> sp;
-        for (size_t k = 0; k < objs.size(); k++) {
-            const DevObject& o = objs[k];
-            if (o.type == 0) {
-                PlaneRec r{};
-                std::memcpy(r.row1, o.inv + 4, 32);
-                r.slot = (int32_t)k;
-                r.key = o.key;
-                pl.push_back(r);
-            } else if (o.type == 1 && o.st) {
-                SphereRec r{};
-                r.m0 = o.inv[0];
-                r.m3 = o.inv[3];
-                r.m5 = o.inv[5];
-                r.m7 = o.inv[7];
-                r.m10 = o.inv[10];
-                r.m11 = o.inv[11];
-                r.m15 = o.inv[15];
-                r.slot = (int32_t)k;
-                r.key = o.key;
-                sp.push_back(r);
-            }
-        }
-        if ((rc = upload(pl, &s->buffers[5], err, err_len)) || (rc = upload(sp, &s->buffers[6], err, err_len))) {
-            ptmi_scene_destroy(s);
-            return rc;
-        }
-        s->dev.planes = (const PlaneRec*)s->buffers[5];
-        s->dev.n_planes = (int32_t)pl.size();
-        s->dev.spheres = (const SphereRec*)s->buffers[6];
-        s->dev.n_spheres_st = (int32_t)sp.size();
-    }
-    // HIP failures from here on release the half-built scene.
-#define SCENE_TRY(call)                                                                            \
-    do {                                                                                           \
-        hipError_t e_ = (call);                                                                    \
-        if (e_ != hipSuccess) {                                                                    \
-            set_err(err, err_len, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
-                    __LINE__);                                                                     \
-            ptmi_scene_destroy(s);                                                                 \
-            return PTMI_ERR_HIP;                                                                   \
-        }                                                                                          \
-    } while (0)
-    if (!objs.empty()) {
-        SCENE_TRY(launch_plane_normals((DevObject*)s->buffers[0], (int)objs.size(), nullptr));
-        SCENE_TRY(hipDeviceSynchronize());
-    }
-    s->dev.roots = (const int32_t*)s->buffers[1];
-    s->dev.nodes = (const DevNode*)s->buffers[2];
-    s->dev.tris = (const DevTri*)s->buffers[3];
-    s->dev.tri_shade = (const DevTriShade*)s->buffers[4];
-    s->dev.nodes4 = (const Node4*)s->buffers[7];
-    s->dev.chains = (const ChainBox*)s->buffers[8];
-    s->dev.root_rec = (const RootRec*)s->buffers[9];
-    s->dev.n_obj = (uint32_t)objs.size();
-    s->dev.n_list = n_obj;
-    s->dev.n_nodes = n_grp;
-    s->dev.n_nodes4 = (int32_t)index.nodes.size();
-    s->dev.n_tri = n_tri;
-    s->dev.cam = cam;
-    hipDeviceProp_t p;
-    SCENE_TRY(hipGetDeviceProperties(&p, device_index));
-    s->resident_waves = p.multiProcessorCount * 16;  // refined below from the occupancy query
-    int blocks_per_cu = 0;
-    const int block = trace_block_threads(s->flags);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, trace_kernel_symbol(s->flags), block, 0) ==
-            hipSuccess &&
-        blocks_per_cu > 0)
-        s->resident_waves = p.multiProcessorCount * blocks_per_cu * (block / 64);
-#undef SCENE_TRY
-    *out = s;
-    return PTMI_OK;
+    return upload_scene(hs, device_index, textures, out, err, err_len);
 }
 
 void ptmi_scene_destroy(ptmi_scene* s) {
@@ -688,55 +718,90 @@ static uint32_t split_point(int g, int n, uint32_t samples) {
     return (uint32_t)std::min<uint64_t>(m, samples);
 }
 
-extern "C" int ptmi_trace_multi(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri, const void* groups,
-                     uint32_t n_grp, const int* devices, uint32_t n_devices, int split, uint32_t samples,
-                     const void* camera, const double* seeds, uint64_t seed_stream, const ptmi_textures* textures,
-                     double* out_rgba, char* err, size_t err_len) {
+extern "C" uint32_t ptmi_sample_split_point(int g, int n, uint32_t samples) {
+    if (n <= 0 || g < 0) return 0;
+    if (g >= n) return samples;
+    return split_point(g, n, samples);
+}
+
+extern "C" int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
+                                      const void* groups, uint32_t n_grp, const int* devices, uint32_t n_devices,
+                                      int split, uint32_t samples, const void* camera, const double* seeds,
+                                      uint64_t seed_stream, const ptmi_textures* textures, double* out_rgba,
+                                      ptmi_multi_timing* timing, char* err, size_t err_len) {
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point a, clk::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const clk::time_point t_start = clk::now();
     if (!out_rgba || samples == 0 || !devices || n_devices == 0 || (split != 0 && split != 1) || !camera) {
         set_err(err, err_len, "ptmi_trace_multi: bad arguments");
         return PTMI_ERR_ARG;
     }
-    const uint32_t W = (uint32_t)rd<int32_t>((const uint8_t*)camera + 0);
-    const uint32_t H = (uint32_t)rd<int32_t>((const uint8_t*)camera + 4);
-    const size_t npix = (size_t)W * H;
-    std::vector<std::vector<double>> part(n_devices);
+    for (uint32_t d = 0; d < n_devices; d++) {
+        const int rc = check_device(devices[d], err, err_len);
+        if (rc) return rc;
+    }
+    // The scene is converted and its traversal index built once, on the host.
+    HostScene hs;
+    int rc = prepare_scene(objects, n_obj, triangles, n_tri, groups, n_grp, camera, textures, hs, err, err_len);
+    if (rc) return rc;
+    const clk::time_point t_prep = clk::now();
+    const size_t npix = (size_t)hs.cam.width * hs.cam.height;
+    const size_t frame_bytes = npix * 4 * sizeof(double);
+    const int root = devices[0];
+    // Device-side combine: every device's partial frame is copied (xGMI peer copy) into
+    // its slot of a gather buffer on the first device, which sums the slots in device
+    // order (deterministic) and normalises (tracer.cl:1184-1187).
+    double* gather = nullptr;
+    HIP_TRY(hipSetDevice(root));
+    HIP_TRY(hipMalloc((void**)&gather, frame_bytes * n_devices));
     std::vector<int> rcs(n_devices, PTMI_OK);
     std::vector<std::string> msgs(n_devices);
+    std::vector<clk::time_point> t_rendered(n_devices, t_prep);
     auto shard = [&](uint32_t d) {
         char e[512] = {0};
-        int& rc = rcs[d];
+        int& drc = rcs[d];
+        const int dev = devices[d];
         ptmi_scene* s = nullptr;
         double *d_seeds = nullptr, *d_sums = nullptr;
         hipStream_t st = nullptr;
-        rc = ptmi_scene_create_textured(devices[d], objects, n_obj, triangles, n_tri, groups, n_grp, camera, textures,
-                                        &s, e, sizeof(e));
-        if (!rc && (s->width != W || s->height != H)) rc = PTMI_ERR_ARG;
-        if (!rc && (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
-                    hipMalloc((void**)&d_seeds, npix * sizeof(double)) != hipSuccess ||
-                    hipMalloc((void**)&d_sums, npix * 4 * sizeof(double)) != hipSuccess)) {
-            rc = PTMI_ERR_HIP;
-            std::snprintf(e, sizeof(e), "device %d: allocation failed", devices[d]);
-        }
-        if (!rc) {
-            if (seeds) {
-                if (hipMemcpyAsync(d_seeds, seeds, npix * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess)
-                    rc = PTMI_ERR_HIP;
-            } else {
-                rc = ptmi_fill_seeds(d_seeds, (uint32_t)npix, seed_stream, st, e, sizeof(e));
+        drc = upload_scene(hs, dev, textures, &s, e, sizeof(e));
+        if (!drc && dev != root) {  // direct xGMI access to the gather buffer where the link allows it
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, dev, root) == hipSuccess && can) {
+                const hipError_t pe = hipDeviceEnablePeerAccess(root, 0);
+                if (pe == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
             }
         }
-        if (!rc) {
+        if (!drc && (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+                     hipMalloc((void**)&d_seeds, npix * sizeof(double)) != hipSuccess ||
+                     hipMalloc((void**)&d_sums, frame_bytes) != hipSuccess)) {
+            drc = PTMI_ERR_HIP;
+            std::snprintf(e, sizeof(e), "device %d: allocation failed", dev);
+        }
+        if (!drc) {
+            if (seeds) {
+                if (hipMemcpyAsync(d_seeds, seeds, npix * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess)
+                    drc = PTMI_ERR_HIP;
+            } else {
+                drc = ptmi_fill_seeds(d_seeds, (uint32_t)npix, seed_stream, st, e, sizeof(e));
+            }
+        }
+        if (!drc) {
             const uint32_t s0 = split == 0 ? split_point(d, n_devices, samples) : 0;
             const uint32_t s1 = split == 0 ? split_point(d + 1, n_devices, samples) : samples;
-            part[d].assign(npix * 4, 0.0);
-            if (s1 > s0)
-                rc = ptmi_scene_render(s, samples, s0, s1, split == 1 ? n_devices : 1, split == 1 ? d : 0, d_seeds,
-                                       d_sums, 0, st, e, sizeof(e));
-            if (!rc && s1 > s0 &&
-                (hipMemcpyAsync(part[d].data(), d_sums, npix * 4 * sizeof(double), hipMemcpyDeviceToHost, st) !=
-                     hipSuccess ||
-                 hipStreamSynchronize(st) != hipSuccess))
-                rc = PTMI_ERR_HIP;
+            // an empty range writes zeros (A = 0), so every slot of the gather buffer is defined
+            drc = ptmi_scene_render(s, samples, s0, s1, split == 1 ? n_devices : 1, split == 1 ? d : 0, d_seeds, d_sums,
+                                    0, st, e, sizeof(e));
+        }
+        if (!drc && hipStreamSynchronize(st) != hipSuccess) drc = PTMI_ERR_HIP;
+        t_rendered[d] = clk::now();
+        if (!drc && (hipMemcpyPeerAsync(gather + (size_t)d * npix * 4, root, d_sums, dev, frame_bytes, st) !=
+                         hipSuccess ||
+                     hipStreamSynchronize(st) != hipSuccess)) {
+            drc = PTMI_ERR_HIP;
+            std::snprintf(e, sizeof(e), "device %d: peer copy to device %d failed", dev, root);
         }
         if (st) (void)hipStreamDestroy(st);
         if (d_seeds) (void)hipFree(d_seeds);
@@ -749,17 +814,40 @@ extern "C" int ptmi_trace_multi(const void* objects, uint32_t n_obj, const void*
     for (auto& t : threads) t.join();
     for (uint32_t d = 0; d < n_devices; d++)
         if (rcs[d]) {
+            (void)hipSetDevice(root);
+            (void)hipFree(gather);
             set_err(err, err_len, "device %d: %s", devices[d], msgs[d].empty() ? "render failed" : msgs[d].c_str());
             return rcs[d];
         }
-    // Sum in device order, then ptmi_finalize's arithmetic (tracer.cl:1184-1187).
-    const double w = 1.0 / samples;
-    for (size_t i = 0; i < npix * 4; i++) {
-        double acc = part[0][i];
-        for (uint32_t d = 1; d < n_devices; d++) acc = acc + part[d][i];
-        out_rgba[i] = (i % 4 == 3) ? 1.0 : acc * w;
+    const clk::time_point t_all_rendered = *std::max_element(t_rendered.begin(), t_rendered.end());
+    HIP_TRY(hipSetDevice(root));
+    double* frame = gather;  // slot 0 is overwritten in place by the ordered sum
+    hipError_t he = launch_combine(gather, n_devices, npix, frame, samples, nullptr);
+    if (he == hipSuccess) he = hipDeviceSynchronize();
+    const clk::time_point t_combined = clk::now();
+    if (he == hipSuccess) he = hipMemcpy(out_rgba, frame, frame_bytes, hipMemcpyDeviceToHost);
+    const clk::time_point t_end = clk::now();
+    (void)hipFree(gather);
+    if (he != hipSuccess) {
+        set_err(err, err_len, "combine / read-back on device %d: %s", root, hipGetErrorString(he));
+        return PTMI_ERR_HIP;
+    }
+    if (timing) {
+        timing->prepare_ms = ms_since(t_start, t_prep);
+        timing->render_ms = ms_since(t_prep, t_all_rendered);
+        timing->combine_ms = ms_since(t_all_rendered, t_combined);
+        timing->readback_ms = ms_since(t_combined, t_end);
+        timing->total_ms = ms_since(t_start, t_end);
     }
     return PTMI_OK;
+}
+
+extern "C" int ptmi_trace_multi(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
+                                const void* groups, uint32_t n_grp, const int* devices, uint32_t n_devices, int split,
+                                uint32_t samples, const void* camera, const double* seeds, uint64_t seed_stream,
+                                const ptmi_textures* textures, double* out_rgba, char* err, size_t err_len) {
+    return ptmi_trace_multi_timed(objects, n_obj, triangles, n_tri, groups, n_grp, devices, n_devices, split, samples,
+                                  camera, seeds, seed_stream, textures, out_rgba, nullptr, err, err_len);
 }
 
 #if PTMI_STATS

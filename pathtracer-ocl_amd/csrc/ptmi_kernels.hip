@@ -1559,6 +1559,28 @@ __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict_
     out[4 * (size_t)i + 3] = 1.0;
 }
 
+// ptmi_trace_multi's device-side combine: out = the partial frames parts[0..nparts)
+// (each npix*4 doubles, RGB sums, A = sample count) summed in part order, times 1/S,
+// alpha 1 (tracer.cl:1184-1187).  out may alias parts[0].
+__global__ __launch_bounds__(256) void combine_kernel(const double* parts, uint32_t nparts, size_t npix,
+                                                      double* out, uint32_t samples) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npix) return;
+    const size_t stride = npix * 4;
+    double r = parts[4 * i], g = parts[4 * i + 1], b = parts[4 * i + 2];
+    for (uint32_t k = 1; k < nparts; k++) {
+        const double* p = parts + k * stride + 4 * i;
+        r = r + p[0];
+        g = g + p[1];
+        b = b + p[2];
+    }
+    const double w = 1.0 / samples;
+    out[4 * i + 0] = r * w;
+    out[4 * i + 1] = g * w;
+    out[4 * i + 2] = b * w;
+    out[4 * i + 3] = 1.0;
+}
+
 // Seeds with Go rand.Float64 granularity (k / 2^53) from a SplitMix64 stream.
 __global__ __launch_bounds__(256) void seeds_kernel(double* __restrict__ seeds, uint32_t n, uint64_t stream) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1622,6 +1644,13 @@ hipError_t launch_reduce(const double* part, double* sums, uint32_t npix, uint32
 
 hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint32_t samples, hipStream_t st) {
     hipLaunchKernelGGL(finalize_kernel, dim3((npix + 255) / 256), dim3(256), 0, st, sums, out, npix, samples);
+    return hipGetLastError();
+}
+
+hipError_t launch_combine(const double* parts, uint32_t nparts, size_t npix, double* out, uint32_t samples,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(combine_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, parts, nparts, npix, out,
+                       samples);
     return hipGetLastError();
 }
 

@@ -132,6 +132,7 @@ int main(int argc, char** argv) {
     std::vector<double> out(n * 4);
     const uint64_t stream =
         c.have_seed ? c.seed : (uint64_t)std::chrono::system_clock::now().time_since_epoch().count();
+    ptmi_multi_timing mt{};
     if (c.gpus == 1) {
         rc = ptmi_trace(r.objects, r.n_obj, r.triangles, r.n_tri, r.groups, r.n_grp, c.device_index,
                         (uint32_t)c.samples, r.camera, nullptr, stream, textured ? &tex : nullptr, out.data(), err,
@@ -139,9 +140,9 @@ int main(int argc, char** argv) {
     } else {
         std::vector<int> devs(c.gpus);
         for (int d = 0; d < c.gpus; d++) devs[d] = d;
-        rc = ptmi_trace_multi(r.objects, r.n_obj, r.triangles, r.n_tri, r.groups, r.n_grp, devs.data(),
-                              (uint32_t)c.gpus, c.split == "tile" ? 1 : 0, (uint32_t)c.samples, r.camera, nullptr,
-                              stream, textured ? &tex : nullptr, out.data(), err, sizeof(err));
+        rc = ptmi_trace_multi_timed(r.objects, r.n_obj, r.triangles, r.n_tri, r.groups, r.n_grp, devs.data(),
+                                    (uint32_t)c.gpus, c.split == "tile" ? 1 : 0, (uint32_t)c.samples, r.camera,
+                                    nullptr, stream, textured ? &tex : nullptr, out.data(), &mt, err, sizeof(err));
     }
     ptmi_host_free_records(&r);
     ptmi_host_free_textures(&tex);
@@ -166,5 +167,9 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "scene %s built in %.3f s; %dx%d x %d spp traced in %.3f s (%.1f Msamples/s); wrote %s\n",
                  scene.c_str(), build_s, c.width, c.height, c.samples, trace_s,
                  (double)n * c.samples / trace_s / 1e6, png.c_str());
+    if (c.gpus > 1)
+        std::fprintf(stderr,
+                     "%d GPUs (%s split): prepare %.3f ms, render %.3f ms, combine %.3f ms, read-back %.3f ms\n",
+                     c.gpus, c.split.c_str(), mt.prepare_ms, mt.render_ms, mt.combine_ms, mt.readback_ms);
     return 0;
 }

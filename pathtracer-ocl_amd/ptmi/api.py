@@ -27,7 +27,16 @@ PTMI_OK, PTMI_ERR_ARG, PTMI_ERR_DEVICE, PTMI_ERR_HIP, PTMI_ERR_UNSUPPORTED, PTMI
 
 EXPORTS = ("ptmi_trace", "ptmi_device_count", "ptmi_device_name", "ptmi_scene_create", "ptmi_scene_destroy",
            "ptmi_scene_size", "ptmi_scene_render", "ptmi_finalize", "ptmi_fill_seeds", "ptmi_build_info",
-           "ptmi_scene_set_timing", "ptmi_scene_kernel_time", "ptmi_trace_multi", "ptmi_scene_create_textured")
+           "ptmi_scene_set_timing", "ptmi_scene_kernel_time", "ptmi_trace_multi", "ptmi_scene_create_textured",
+           "ptmi_trace_multi_timed", "ptmi_sample_split_point")
+
+
+class MultiTiming(ctypes.Structure):
+    """ptmi_multi_timing (include/ptmi.h): wall-clock phases of ptmi_trace_multi, ms."""
+    _fields_ = [(n, ctypes.c_double) for n in ("prepare_ms", "render_ms", "combine_ms", "readback_ms", "total_ms")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
 
 
 class PtmiError(RuntimeError):
@@ -56,6 +65,11 @@ def load_library(path=None):
     lib.ptmi_trace_multi.restype = i32
     lib.ptmi_trace_multi.argtypes = [vp, u32, vp, u32, vp, u32, vp, u32, i32, u32, vp, vp, ctypes.c_uint64, vp, vp,
                                      cp, sz]
+    lib.ptmi_trace_multi_timed.restype = i32
+    lib.ptmi_trace_multi_timed.argtypes = [vp, u32, vp, u32, vp, u32, vp, u32, i32, u32, vp, vp, ctypes.c_uint64, vp,
+                                           vp, ctypes.POINTER(MultiTiming), cp, sz]
+    lib.ptmi_sample_split_point.restype = u32
+    lib.ptmi_sample_split_point.argtypes = [i32, i32, u32]
     lib.ptmi_device_count.restype = i32
     lib.ptmi_device_count.argtypes = []
     lib.ptmi_device_name.restype = i32
@@ -142,6 +156,38 @@ def Trace(objects, triangles, groups, deviceIndex, samples, camera, textures=Non
                         out.ctypes.data_as(ctypes.c_void_p), err, len(err))
     _check(rc, err)
     return out
+
+
+def TraceMulti(objects, triangles, groups, devices, split, samples, camera, textures=None, sphereTextures=None,
+               cubeTextures=None, seeds=None, seed_stream=0):
+    """ptmi_trace_multi_timed: the frame over `devices` (an index may repeat) with a
+    sample (split="sample") or 8x8-tile (split="tile") split, combined on device.
+    Returns (float64 RGBA of len W*H*4, {phase: ms})."""
+    tex = TextureSet(textures, sphereTextures, cubeTextures)
+    lib = load_library()
+    objects, triangles, groups, camera = _records(objects, triangles, groups, camera)
+    w, h = int(camera["width"][0]), int(camera["height"][0])
+    if seeds is not None:
+        seeds = np.ascontiguousarray(seeds, dtype=np.float64)
+        if seeds.size != w * h:
+            raise ValueError("seeds: expected %d values, got %d" % (w * h, seeds.size))
+    if split not in ("sample", "tile"):
+        raise ValueError("split must be 'sample' or 'tile'")
+    devs = (ctypes.c_int * len(devices))(*devices)
+    out = np.empty(w * h * 4, dtype=np.float64)
+    timing = MultiTiming()
+    err = ctypes.create_string_buffer(1024)
+    rc = lib.ptmi_trace_multi_timed(_ptr(objects), len(objects), _ptr(triangles), len(triangles), _ptr(groups),
+                                    len(groups), devs, len(devices), 0 if split == "sample" else 1, int(samples),
+                                    _ptr(camera), _ptr(seeds), int(seed_stream), tex.pointer(),
+                                    out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(timing), err, len(err))
+    _check(rc, err)
+    return out, timing.as_dict()
+
+
+def sample_split_point(g, n, samples):
+    """The library's cost-balanced sample split (ptmi_sample_split_point)."""
+    return load_library().ptmi_sample_split_point(int(g), int(n), int(samples))
 
 
 class Scene:

@@ -157,3 +157,13 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "..", "bench.py"), "--gpus", "4"],
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 7, 8])
+@pytest.mark.parametrize("samples", [1, 5, 300, 553, 731, 1500, 2048, 4096])
+def test_library_and_python_sample_splits_agree(world, samples):
+    """ptmi_trace_multi's split (C++ split_point, exported as ptmi_sample_split_point)
+    and bench.py's ranks (ptmi/dist.py sample_split_point) are the same table."""
+    from ptmi import api
+    for g in range(world + 1):
+        assert api.sample_split_point(g, world, samples) == pdist.sample_split_point(g, world, samples), (g, world)

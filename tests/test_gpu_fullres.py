@@ -103,3 +103,21 @@ def test_eight_gpu_shards_sum_to_frame_at_full_resolution(scene, ap, fl, split):
         assert torch.equal(acc, full)
     else:
         assert (acc - full).abs().max().item() < 1e-12 * S
+
+
+@pytest.mark.parametrize("split", ["sample", "tile"])
+def test_trace_multi_full_frame_device_combine(split):
+    """ptmi_trace_multi at 1280x960 over 8 device slots (device 0 repeated on this
+    box): equal to ptmi_trace, and the device-side combine of eight 39 MB partial
+    frames (peer copies + ordered sum on the first device) stays in milliseconds."""
+    W, H, S = 1280, 960, 16
+    objs, tris, grps, cam = scene_inputs("reference", W, H)
+    seeds = layout.seeds_go_float64(W * H, 1234)
+    single = api.Trace(objs, tris, grps, 0, S, cam, seeds=seeds)
+    out, timing = api.TraceMulti(objs, tris, grps, [0] * 8, split, S, cam, seeds=seeds)
+    print("ptmi_trace_multi 8 x device 0, %s split: %s" % (split, {k: round(v, 3) for k, v in timing.items()}))
+    if split == "tile":
+        assert np.array_equal(out, single)
+    else:
+        assert np.abs(out - single).max() < 1e-12
+    assert timing["combine_ms"] < 20.0, timing

@@ -260,27 +260,23 @@ def test_cpu_oracle_matches_live_reference_materials(scene, ap):
 
 
 
-@pytest.mark.parametrize("scene,split,ndev", [("reference", 1, 2), ("teapot", 1, 3), ("reference", 0, 2),
-                                              ("transparency", 0, 3)])
-def test_trace_multi_matches_single_device(scene, split, ndev):
-    """ptmi_trace_multi with device 0 repeated (this box has one GPU): the tile
-    split is bit-identical to ptmi_trace, the sample split equal up to FP64
-    summation order."""
-    import ctypes
-    w, h, spp = 40, 24, 5
+@pytest.mark.parametrize("scene,w,h,spp,split,ndev", [("reference", 40, 24, 5, "tile", 2),
+                                                       ("teapot", 40, 24, 5, "tile", 3),
+                                                       ("reference", 40, 24, 5, "sample", 2),
+                                                       ("transparency", 40, 24, 5, "sample", 3),
+                                                       ("reference", 8, 8, 1500, "sample", 8),
+                                                       ("gopher", 64, 48, 4, "tile", 8)])
+def test_trace_multi_matches_single_device(scene, w, h, spp, split, ndev):
+    """ptmi_trace_multi with device 0 repeated (this box has one GPU): host scene
+    prepared once, device-side combine (peer copies into a gather buffer, ordered sum).
+    The tile split is bit-identical to ptmi_trace, the sample split equal up to FP64
+    summation order; 1500 spp over 8 devices crosses both cost knots of the split."""
     objs, tris, grps, cam = scene_inputs(scene, w, h)
     seeds = layout.seeds_go_float64(w * h, 61)
     single = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
-    lib = api.load_library()
-    devs = (ctypes.c_int * ndev)(*([0] * ndev))
-    out = np.empty(w * h * 4)
-    err = ctypes.create_string_buffer(512)
-    cam1 = np.asarray(cam).reshape(1)
-    rc = lib.ptmi_trace_multi(objs.ctypes.data, len(objs), tris.ctypes.data if len(tris) else None, len(tris),
-                              grps.ctypes.data if len(grps) else None, len(grps), devs, ndev, split, spp,
-                              cam1.ctypes.data, seeds.ctypes.data, 0, None, out.ctypes.data, err, 512)
-    assert rc == 0, err.value
-    if split == 1:
+    out, timing = api.TraceMulti(objs, tris, grps, [0] * ndev, split, spp, cam, seeds=seeds)
+    if split == "tile":
         assert np.array_equal(out, single)
     else:
         assert np.abs(out - single).max() < 1e-12
+    assert all(timing[k] >= 0 for k in timing) and timing["total_ms"] >= timing["render_ms"]
