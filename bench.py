@@ -295,7 +295,7 @@ def main():
         # Go caller of ocl.Trace sees (SURVEY.md 8d t_trace).
         inclusive = None
         if world == 1 and not args.no_trace_call:
-            api.Trace(objs, tris, grps, device, 1, cam, seeds=seeds_host)  # host-side warm-up (page-in, pinning)
+            api.Trace(objs, tris, grps, device, S, cam, seeds=seeds_host)  # warm-up: host page-in, allocator
             t0 = time.perf_counter()
             api.Trace(objs, tris, grps, device, S, cam, seeds=seeds_host)
             t_call = time.perf_counter() - t0

@@ -1312,8 +1312,9 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
 // Writes the chunk's RGB sums (A = #samples) to out[(chunk*npix + pixel)*4].
 template <int FL>
 #ifndef PTMI_WAVES
-#define PTMI_WAVES 5        // waves/SIMD the register allocation targets (scenes without groups): 96 VGPRs
-                            // with 64 B/lane of spilled loop invariants beat 4 waves without (C2 -1.3 %, C3 -2.9 %)
+#define PTMI_WAVES 3        // waves/SIMD the register allocation targets (scenes without groups).  The kernel is
+                            // VALU-issue bound: C2 2048 spp 186.3 ms at 3 (no spill) vs 189.0 at 5 (96 VGPRs +
+                            // 80 B/lane of spilled loop invariants) and 186.3 at 2; C3 flat (196.3 vs 195.9)
 #endif
 #ifndef PTMI_WAVES_GROUPS
 #define PTMI_WAVES_GROUPS 3  // ... and with BVH groups (the walk needs more registers; 4 spills)

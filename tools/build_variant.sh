@@ -1,0 +1,19 @@
+# DIAGNOSTIC: build an experimental libptmi.so from the working tree with extra
+# defines.  usage: bash tools/build_variant.sh <name> [-DNAME=VAL ...]
+#   -> pathtracer-ocl_amd/build/exp/libptmi_<name>.so   (tools/exp_variants.sh times it)
+# <name> = head: the HEAD commit's sources instead of the working tree.
+set -e
+NAME=$1; shift
+cd "$(dirname "$0")/../pathtracer-ocl_amd"
+mkdir -p build/exp
+SRC=csrc
+if [ "$NAME" = head ]; then
+  SRC=$(mktemp -d)/csrc; mkdir -p $SRC
+  for f in ptmi_kernels.hip ptmi_api.cpp ptmi_bvh.cpp ptmi_bvh.h ptmi_device.h ptmi_sinf.h ptmi_fp64core.h; do
+    git show HEAD:pathtracer-ocl_amd/csrc/$f > $SRC/$f
+  done
+  cp -r ../include $(dirname $SRC)/../include 2>/dev/null || true
+  git show HEAD:include/ptmi.h > $(dirname $SRC)/../include/ptmi.h
+fi
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wno-unused-result \
+  "$@" -shared -o build/exp/libptmi_$NAME.so $SRC/ptmi_kernels.hip $SRC/ptmi_api.cpp $SRC/ptmi_bvh.cpp
