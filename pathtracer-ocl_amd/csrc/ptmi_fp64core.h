@@ -17,15 +17,22 @@ namespace ptmi {
 // says why).  tests/test_gpu_rng.py checks the cores against
 // the compiler's operators, and tests/test_gpu_parity.py the affine images against
 // the generic instantiation, which keeps the full expansions.
-__device__ __forceinline__ double div_core(double x, double y) {  // x / y: v_div_fmas with vcc = 0, no fix-up
+// The divide core in two steps: the Newton-refined reciprocal depends on y alone, so
+// quotients with one denominator can share it (sphere roots) and stay bit-identical.
+__device__ __forceinline__ double rcp_core(double y) {
     double r = __builtin_amdgcn_rcp(y);
     double e = fma(-y, r, 1.0);
     r = fma(r, e, r);
     e = fma(-y, r, 1.0);
-    r = fma(r, e, r);
+    return fma(r, e, r);
+}
+__device__ __forceinline__ double div_core_r(double x, double y, double r) {  // r = rcp_core(y)
     const double q = x * r;
     const double rem = fma(-y, q, x);
     return fma(rem, r, q);
+}
+__device__ __forceinline__ double div_core(double x, double y) {  // x / y: v_div_fmas with vcc = 0, no fix-up
+    return div_core_r(x, y, rcp_core(y));
 }
 __device__ __forceinline__ double sqrt_core(double x) {  // sqrt(x) for x in [2^-767, 2^1023]
     const double r = __builtin_amdgcn_rsq(x);

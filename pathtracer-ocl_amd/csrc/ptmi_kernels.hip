@@ -98,6 +98,12 @@ static constexpr int kRefillNeed = PTMI_REFILL_NEED;
 #define PTMI_WALK_BATCH 24
 #endif
 static constexpr int kWalkBatch = PTMI_WALK_BATCH;  // parked lanes that trigger a wave's BVH walk phase
+#ifndef PTMI_SPHERE_RCP
+#define PTMI_SPHERE_RCP 1  // both sphere roots from one reciprocal (sphere_roots)
+#endif
+#ifndef PTMI_SPHERE_DEFER
+#define PTMI_SPHERE_DEFER 1  // sphere roots evaluated once per lane after the loop (find_closest_prims)
+#endif
 
 struct d4 {
     double x, y, z, w;
@@ -576,10 +582,17 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
     int sp = 0;
     int cur = R.entry;
     PTMI_COUNT(0);
+#if PTMI_STATS == 1
+    int st_nodes = 0, st_leaves = 0;
+    const double st_t0 = h.t;
+#endif
     while (true) {
         PTMI_COUNT_ACTIVE(19);  // (stats: wave-level walk loop iterations)
         if (cur >= 0) {
             PTMI_COUNT(1);
+#if PTMI_STATS == 1
+            st_nodes++;
+#endif
             // The node's 112 B as seven 16-B loads issued together (one wait), from LDS
             // for the first kLdsNodes Node4s (the top levels, ptmi_bvh.cpp), else global.
             const float4* src = cur < kLdsNodes ? reinterpret_cast<const float4*>(lds_nodes) + 7 * cur
@@ -631,6 +644,9 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
             const int code = -cur - 1;
             const int first = code >> 3, end = first + (code & 7);
             PTMI_COUNT(2);
+#if PTMI_STATS == 1
+            st_leaves++;
+#endif
             for (int i = first; i < end; i++) {
                 PTMI_COUNT(3);
 #if !(defined(PTMI_EXP) && (PTMI_EXP & 4))
@@ -641,6 +657,11 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
         if (sp == 0) break;
         cur = stk[(--sp) * kStkStride];
     }
+#if PTMI_STATS == 1
+    if (st_leaves == 0) PTMI_COUNT(20);  // (stats: walks that reach no leaf)
+    if (st_leaves == 0 && st_nodes <= 1) PTMI_COUNT(21);  // (... that end at the root node)
+    if (h.t < st_t0) PTMI_COUNT(22);  // (... that improve the best hit)
+#endif
 }
 
 // Candidate update as selects (no exec-mask branching).  t > EPSILON implies
@@ -671,6 +692,20 @@ __device__ __forceinline__ void sphere_quad(d4 o, d4 d, double& a, double& b, do
 // >= 2^-767 or so small that b is too (then both roots are below EPSILON).
 template <bool A>
 __device__ __forceinline__ void sphere_roots(Hit& h, double a, double b, double disc, int slot, int key) {
+    if (A && PTMI_SPHERE_RCP && !(PTMI_ABLATE & 128)) {
+        // Both roots from one reciprocal of 2a (div_core_r: bit-identical to two div_core
+        // calls), then one candidate: t1 if it is one, else t2 -- the reference records
+        // both, and t2 >= t1 can only win when t1 <= EPSILON (see below).
+        if (disc > 0.0) {
+            const double sq = sqrt_core(disc);
+            const double y = 2 * a;
+            const double r = rcp_core(y);
+            const double t1 = div_core_r(-b - sq, y, r);
+            const double t2 = div_core_r(-b + sq, y, r);
+            consider_sel(h, t1 > kEps ? t1 : t2, slot, key);
+        }
+        return;
+    }
     if (disc > 0.0) {
         // a > 0 and sq >= 0 give t1 <= t2 after rounding (rounding is monotonic),
         // so t2 can only be recorded as the winner when t1 itself is not a
@@ -709,16 +744,25 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     const int np = (PTMI_ABLATE & 8) ? 0 : S.n_planes;
     // intersectPlane (478-483): row 1 only.  Planes are taken two at a time so the
     // two independent division chains overlap (then one odd plane).
-    auto plane_t = [&](const PlaneRec& P, double& q, bool& ok) {
-        const double oy = ((P.row1[0] * ro.x + P.row1[1] * ro.y) + P.row1[2] * ro.z) + (A ? P.row1[3] : P.row1[3] * ro.w);
-        const double dy0 = (P.row1[0] * rd.x + P.row1[1] * rd.y) + P.row1[2] * rd.z;
-        const double dy = A ? dy0 : dy0 + P.row1[3] * rd.w;
+    // Row 1 of mul() for the plane's origin and direction (intersectPlane, 478-483).
+    auto plane_rows = [&](const PlaneRec& P, double& oy, double& dy) {
+        const double* m = P.row1;
+        oy = ((m[0] * ro.x + m[1] * ro.y) + m[2] * ro.z) + (A ? m[3] : m[3] * ro.w);
+        const double dy0 = (m[0] * rd.x + m[1] * rd.y) + m[2] * rd.z;
+        dy = A ? dy0 : dy0 + m[3] * rd.w;
+    };
+    auto plane_q = [&](double oy, double dy, double& q, bool& ok) {
         // Affine: the divide core.  Its range steps act only when |dy| is denormal or
         // above 2^1022, -oy is below 2^-970, or the quotient is denormal or above 2^767;
         // then q <= EPSILON, |dy| <= EPSILON, or q >= 1024 under both arithmetics, and
         // the plane is not taken either way.
         q = (PTMI_ABLATE & 64) ? -oy * __builtin_amdgcn_rcp(dy) : A ? div_core(-oy, dy) : -oy / dy;  // DIAGNOSTIC 64
         ok = (fabs(dy) > kEps) & (q > kEps);
+    };
+    auto plane_t = [&](const PlaneRec& P, double& q, bool& ok) {
+        double oy, dy;
+        plane_rows(P, oy, dy);
+        plane_q(oy, dy, q, ok);
     };
     auto plane_take = [&](const PlaneRec& P, double q, bool ok) {
         const bool c = ok & (q < h.t);
@@ -728,10 +772,12 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     int p = 0;
     for (; p + 1 < np; p += 2) {
         const PlaneRec P0 = S.planes[p], P1 = S.planes[p + 1];
-        double q0, q1;
+        double oy0, dy0, oy1, dy1, q0, q1;
         bool k0, k1;
-        plane_t(P0, q0, k0);
-        plane_t(P1, q1, k1);
+        plane_rows(P0, oy0, dy0);
+        plane_rows(P1, oy1, dy1);
+        plane_q(oy0, dy0, q0, k0);
+        plane_q(oy1, dy1, q1, k1);
         plane_take(P0, q0, k0);
         plane_take(P1, q1, k1);
     }
@@ -752,6 +798,30 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
             d = mk(Q.m0 * rd.x + Q.m3 * rd.w, Q.m5 * rd.y + Q.m7 * rd.w, Q.m10 * rd.z + Q.m11 * rd.w, Q.m15 * rd.w);
         }
     };
+    // A ray's line meets few spheres (disc > 0 in ~5 % of the tests), yet a wave of 64
+    // rays almost always has one lane that does: evaluated in place, the root code would
+    // run for every sphere.  Each lane instead keeps its first sphere with disc > 0 and
+    // evaluates the roots once after the loop (a second such sphere -- rare -- in place).
+    // The candidates are the same and the winner is their lexicographic minimum
+    // (better()), so the order of evaluation does not matter.
+    bool pend = false;
+    double pa = 0.0, pb = 0.0, pd = 0.0;
+    int pslot = 0, pkey = 0;
+    auto defer = [&](double a, double b, double disc, int slot, int key) {
+        if (!PTMI_SPHERE_DEFER) {
+            sphere_roots<A>(h, a, b, disc, slot, key);
+            return;
+        }
+        const bool has = disc > 0.0;
+        if (has && pend) sphere_roots<A>(h, a, b, disc, slot, key);
+        const bool take = has && !pend;
+        pa = take ? a : pa;
+        pb = take ? b : pb;
+        pd = take ? disc : pd;
+        pslot = take ? slot : pslot;
+        pkey = take ? key : pkey;
+        pend = pend || has;
+    };
     int q = 0;
     for (; q + 1 < nq; q += 2) {  // two spheres at a time: overlapping quadratic setups
         const SphereRec Q0 = S.spheres[q], Q1 = S.spheres[q + 1];
@@ -761,15 +831,18 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         double a0, b0, disc0, a1, b1, disc1;
         sphere_quad<A>(o0, d0, a0, b0, disc0);
         sphere_quad<A>(o1, d1, a1, b1, disc1);
-        sphere_roots<A>(h, a0, b0, disc0, Q0.slot, Q0.key);
-        sphere_roots<A>(h, a1, b1, disc1, Q1.slot, Q1.key);
+        defer(a0, b0, disc0, Q0.slot, Q0.key);
+        defer(a1, b1, disc1, Q1.slot, Q1.key);
     }
     if (q < nq) {
         const SphereRec Q0 = S.spheres[q];
         d4 o0, d0;
         sphere_ray(Q0, o0, d0);
-        sphere_test<A>(h, o0, d0, Q0.slot, Q0.key);
+        double a0, b0, disc0;
+        sphere_quad<A>(o0, d0, a0, b0, disc0);
+        defer(a0, b0, disc0, Q0.slot, Q0.key);
     }
+    if (pend) sphere_roots<A>(h, pa, pb, pd, pslot, pkey);
     int j = S.run_end[0];
     for (; j < S.run_end[1]; j++) {  // spheres with other matrices
         const DevObject& ob = S.objs[j];

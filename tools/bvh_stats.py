@@ -26,7 +26,7 @@ lib.ptmi_stats_read(buf, 1)
 names = ["walks", "node4", "leaves", "tri_tests", "verifies", "gate_rejects", "obj_gate_pass", "group_obj_tests",
          "walk_phases", "lanes_in_phases", "wave_iterations", "eager_rewalks",
          "cyc_refill", "cyc_prims_gate", "cyc_walk_phases", "cyc_shade", "cyc_loop", "exact_chain_verifies",
-         "cyc_walk_loops", "walk_loop_wave_iters"]
+         "cyc_walk_loops", "walk_loop_wave_iters", "walks_no_leaf", "walks_root_only", "walks_improving"]
 v = dict(zip(names, buf))
 n = W * H * spp
 print(scene, "spp", spp)
