@@ -34,6 +34,8 @@ hipError_t launch_combine(const double* parts, uint32_t nparts, size_t npix, dou
                           hipStream_t st);
 const void* trace_kernel_symbol(int flags);
 int trace_block_threads(int flags);
+int trace_tiles_per_block(int flags);
+int watchdog_fired(bool clear);
 }  // namespace ptmi
 
 using namespace ptmi;
@@ -324,6 +326,12 @@ int prepare_scene(const void* objects, uint32_t n_obj, const void* triangles, ui
     for (const DevObject& o : hs.objs)
         if ((o.tex && (o.type == 0 || o.type == 1 || o.type == 3)) || (o.tex_nm && o.type == 0)) flags = 63;
     if (const char* f = getenv("PTMI_FORCE_FLAGS")) flags = atoi(f) & 63;  // testing: force the generic path
+    // BVH scenes run trace_kernel's in-wave walks; PTMI_WALKER=1 selects the walker-wave
+    // kernel (trace_kernel_ww: measured slower, kept for A/B measurement).
+    {
+        const char* w = getenv("PTMI_WALKER");
+        if (!(w && atoi(w) == 1)) flags |= 64;
+    }
     if (textures) {
         for (int k = 0; k < 3; k++) {
             const uint64_t texels = (uint64_t)textures->width[k] * textures->height[k] * textures->count[k];
@@ -446,7 +454,7 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, trace_kernel_symbol(s->flags), block, 0) ==
             hipSuccess &&
         blocks_per_cu > 0)
-        s->resident_waves = p.multiProcessorCount * blocks_per_cu * (block / 64);
+        s->resident_waves = p.multiProcessorCount * blocks_per_cu * trace_tiles_per_block(s->flags);  // tile waves
 #undef SCENE_TRY
     *out = s;
     return PTMI_OK;
@@ -690,6 +698,10 @@ int ptmi_trace(const void* objects, uint32_t n_obj, const void* triangles, uint3
     TRY_OR_FAIL(hipMemcpyAsync(out_rgba, d_sums, (size_t)npix * 4 * sizeof(double), hipMemcpyDeviceToHost, st));
     TRY_OR_FAIL(hipStreamSynchronize(st));
 #undef TRY_OR_FAIL
+    if (watchdog_fired(true) > 0) {
+        set_err(err, err_len, "trace kernel watchdog fired (a wave exceeded its loop bound); the frame is invalid");
+        return fail(PTMI_ERR_HIP);
+    }
     fail(PTMI_OK);
     return PTMI_OK;
 }
@@ -828,6 +840,13 @@ extern "C" int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const
     if (he == hipSuccess) he = hipMemcpy(out_rgba, frame, frame_bytes, hipMemcpyDeviceToHost);
     const clk::time_point t_end = clk::now();
     (void)hipFree(gather);
+    for (uint32_t d = 0; d < n_devices; d++) {
+        (void)hipSetDevice(devices[d]);
+        if (watchdog_fired(true) > 0) {
+            set_err(err, err_len, "device %d: trace kernel watchdog fired; the frame is invalid", devices[d]);
+            return PTMI_ERR_HIP;
+        }
+    }
     if (he != hipSuccess) {
         set_err(err, err_len, "combine / read-back on device %d: %s", root, hipGetErrorString(he));
         return PTMI_ERR_HIP;

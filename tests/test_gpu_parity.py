@@ -280,3 +280,17 @@ def test_trace_multi_matches_single_device(scene, w, h, spp, split, ndev):
     else:
         assert np.abs(out - single).max() < 1e-12
     assert all(timing[k] >= 0 for k in timing) and timing["total_ms"] >= timing["render_ms"]
+
+
+@pytest.mark.parametrize("scene,w,h,spp,ap", [("teapot", 96, 64, 5, 0.0), ("gopher", 80, 64, 4, 0.0),
+                                              ("teapot", 64, 48, 3, 0.15), ("christian", 64, 48, 3, 0.0),
+                                              ("transparent_teapot", 64, 48, 4, 0.0)])
+def test_walker_waves_match_in_wave_walks(monkeypatch, scene, w, h, spp, ap):
+    """BVH scenes: the walker-wave kernel (trace_kernel_ww, PTMI_WALKER=1) and
+    trace_kernel's in-wave walks (the default) give bit-identical images."""
+    objs, tris, grps, cam = scene_inputs(scene, w, h, ap, 1.6 if ap else 0.0)
+    seeds = layout.seeds_go_float64(w * h, 404)
+    inwave = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    monkeypatch.setenv("PTMI_WALKER", "1")
+    ww = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    assert np.array_equal(ww, inwave)
