@@ -35,7 +35,6 @@ hipError_t launch_combine(const double* parts, uint32_t nparts, size_t npix, dou
 const void* trace_kernel_symbol(int flags);
 int trace_block_threads(int flags);
 int trace_tiles_per_block(int flags);
-int watchdog_fired(bool clear);
 }  // namespace ptmi
 
 using namespace ptmi;
@@ -326,12 +325,6 @@ int prepare_scene(const void* objects, uint32_t n_obj, const void* triangles, ui
     for (const DevObject& o : hs.objs)
         if ((o.tex && (o.type == 0 || o.type == 1 || o.type == 3)) || (o.tex_nm && o.type == 0)) flags = 63;
     if (const char* f = getenv("PTMI_FORCE_FLAGS")) flags = atoi(f) & 63;  // testing: force the generic path
-    // BVH scenes run trace_kernel's in-wave walks; PTMI_WALKER=1 selects the walker-wave
-    // kernel (trace_kernel_ww: measured slower, kept for A/B measurement).
-    {
-        const char* w = getenv("PTMI_WALKER");
-        if (!(w && atoi(w) == 1)) flags |= 64;
-    }
     if (textures) {
         for (int k = 0; k < 3; k++) {
             const uint64_t texels = (uint64_t)textures->width[k] * textures->height[k] * textures->count[k];
@@ -416,6 +409,11 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     for (int t = 0; t < 5; t++) s->dev.run_end[t] = hs.run_end[t];
     s->dev.planes = (const PlaneRec*)s->buffers[5];
     s->dev.n_planes = (int32_t)hs.planes.size();
+    // the leading planes (list order kept) whose row 1 has +-0 x and z entries
+    s->dev.n_planes_y = 0;
+    while (s->dev.n_planes_y < s->dev.n_planes && hs.planes[s->dev.n_planes_y].row1[0] == 0.0 &&
+           hs.planes[s->dev.n_planes_y].row1[2] == 0.0)
+        s->dev.n_planes_y++;
     s->dev.spheres = (const SphereRec*)s->buffers[6];
     s->dev.n_spheres_st = (int32_t)hs.spheres.size();
     // HIP failures from here on release the half-built scene.
@@ -444,6 +442,7 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     s->dev.n_list = hs.n_list;
     s->dev.n_nodes = hs.n_grp;
     s->dev.n_nodes4 = (int32_t)hs.index.nodes.size();
+    s->dev.steal = getenv("PTMI_NO_STEAL") ? 0u : 1u;  // testing: per-lane sample order as without stealing
     s->dev.n_tri = hs.n_tri;
     s->dev.cam = hs.cam;
     hipDeviceProp_t p;
@@ -698,10 +697,6 @@ int ptmi_trace(const void* objects, uint32_t n_obj, const void* triangles, uint3
     TRY_OR_FAIL(hipMemcpyAsync(out_rgba, d_sums, (size_t)npix * 4 * sizeof(double), hipMemcpyDeviceToHost, st));
     TRY_OR_FAIL(hipStreamSynchronize(st));
 #undef TRY_OR_FAIL
-    if (watchdog_fired(true) > 0) {
-        set_err(err, err_len, "trace kernel watchdog fired (a wave exceeded its loop bound); the frame is invalid");
-        return fail(PTMI_ERR_HIP);
-    }
     fail(PTMI_OK);
     return PTMI_OK;
 }
@@ -840,13 +835,6 @@ extern "C" int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const
     if (he == hipSuccess) he = hipMemcpy(out_rgba, frame, frame_bytes, hipMemcpyDeviceToHost);
     const clk::time_point t_end = clk::now();
     (void)hipFree(gather);
-    for (uint32_t d = 0; d < n_devices; d++) {
-        (void)hipSetDevice(devices[d]);
-        if (watchdog_fired(true) > 0) {
-            set_err(err, err_len, "device %d: trace kernel watchdog fired; the frame is invalid", devices[d]);
-            return PTMI_ERR_HIP;
-        }
-    }
     if (he != hipSuccess) {
         set_err(err, err_len, "combine / read-back on device %d: %s", root, hipGetErrorString(he));
         return PTMI_ERR_HIP;

@@ -133,6 +133,7 @@ struct DevScene {
     const DevObject* objs;
     int32_t run_end[5];  // slots [run_end[t-1], run_end[t]) hold type t
     int32_t n_planes;
+    int32_t n_planes_y;  // leading planes whose row 1 is (+-0, m1, +-0, m3) (find_closest_prims)
     const PlaneRec* planes;      // all planes
     const SphereRec* spheres;    // scale+translate spheres (the rest: DevObject path)
     int32_t n_spheres_st;
@@ -147,6 +148,7 @@ struct DevScene {
     uint32_t n_obj;   // intersectable objects in objs[]
     uint32_t n_nodes, n_tri;
     uint32_t n_list;  // numObjects of the reference's list (fgi = seed / numObjects, tracer.cl:840)
+    uint32_t steal;   // segment stealing in BVH scenes (trace_kernel); 0: off (PTMI_NO_STEAL, A/B and tests)
     DevCamera cam;
     DevTexArray tex[3];  // textures, sphereTextures, cubeMapTextures (tracer.cl:833)
 };

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "ptmi_device.h"
 #include "ptmi_sinf.h"
 #include "ptmi_fp64core.h"
@@ -37,11 +39,11 @@
 // re-walks [12..16] shader-clock cycles in refill / closest-prims+gate / walk phases /
 // shade / whole loop [17] exact chain verifications [18] cycles in walk loops
 // [19] wave-level walk loop iterations.
-__device__ unsigned long long ptmi_stats[40];  // [24..39]: walker-wave counters (trace_kernel_ww)
+__device__ unsigned long long ptmi_stats[40];
 // Per-wave accumulators (one writer per wave: the first active lane), flushed to
 // ptmi_stats with one atomic per counter when the wave leaves its loop, so clock
 // and per-wave counts do not serialise on global atomics.
-__shared__ unsigned long long ptmi_wstat[4][24];
+__shared__ unsigned long long ptmi_wstat[4][32];
 #define PTMI_FIRST_ACTIVE() ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1)
 #define PTMI_WADD(i, v)                                                \
     do {                                                               \
@@ -98,6 +100,13 @@ static constexpr int kRefillNeed = PTMI_REFILL_NEED;
 #define PTMI_WALK_BATCH 24
 #endif
 static constexpr int kWalkBatch = PTMI_WALK_BATCH;  // parked lanes that trigger a wave's BVH walk phase
+#ifndef PTMI_STEAL
+#define PTMI_STEAL 1  // finished lanes take over samples of busy lanes of the wave (trace_kernel)
+#endif
+#ifndef PTMI_STEAL_MIN
+#define PTMI_STEAL_MIN 2  // a lane is stolen from when it has at least this many samples not started
+#endif
+static constexpr uint32_t kStealMin = PTMI_STEAL_MIN;
 #ifndef PTMI_SPHERE_RCP
 #define PTMI_SPHERE_RCP 1  // both sphere roots from one reciprocal (sphere_roots)
 #endif
@@ -588,6 +597,7 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
 #endif
     while (true) {
         PTMI_COUNT_ACTIVE(19);  // (stats: wave-level walk loop iterations)
+        PTMI_TSTAMP(t_nd);
         if (cur >= 0) {
             PTMI_COUNT(1);
 #if PTMI_STATS == 1
@@ -636,11 +646,14 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
             if (k[3] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[3];
             if (k[2] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[2];
             if (k[1] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[1];
+            PTMI_TADD(29, t_nd);
             if (k[0] < __builtin_huge_valf()) {
                 cur = c[0];
                 continue;
             }
         } else if (cur != kEmptyChild) {
+            PTMI_TSTAMP(t_lf);
+            PTMI_WADD(31, 1ull);
             const int code = -cur - 1;
             const int first = code >> 3, end = first + (code & 7);
             PTMI_COUNT(2);
@@ -653,6 +666,7 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
                 tri_test<kVerify>(S, S.tris[i], o, d, slot, key, h, vchain);
 #endif
             }
+            PTMI_TADD(30, t_lf);
         }
         if (sp == 0) break;
         cur = stk[(--sp) * kStkStride];
@@ -730,6 +744,29 @@ __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int ke
     sphere_roots<A>(h, a, b, disc, slot, key);
 }
 
+// Row 1 of mul() for a plane's origin and direction (intersectPlane, tracer.cl:478-483),
+// affine case, with the +-0 entries of row1[0..2] (bit i of NZ clear) skipped: for a
+// finite ray such a term adds an exact +-0, so the remaining terms, summed in the
+// reference's order, give oy and dy bit for bit up to the sign of an exact zero, which
+// neither t = -oy / dy nor its tests observe (t is then +-0, or |dy| is below EPSILON).
+// The walls of the reference scenes have one or two such zeros.
+template <int NZ>
+__device__ __forceinline__ void plane_rows_nz(const double* __restrict__ m, d4 ro, d4 rd, double& oy, double& dy) {
+    static_assert(NZ >= 1 && NZ <= 7, "at least one live term");
+    double o = 0.0, d = 0.0;
+    bool any = false;
+    auto term = [&](double mi, double x, double dx) {
+        o = any ? o + mi * x : mi * x;
+        d = any ? d + mi * dx : mi * dx;
+        any = true;
+    };
+    if constexpr ((NZ & 1) != 0) term(m[0], ro.x, rd.x);
+    if constexpr ((NZ & 2) != 0) term(m[1], ro.y, rd.y);
+    if constexpr ((NZ & 4) != 0) term(m[2], ro.z, rd.z);
+    oy = o + m[3];
+    dy = d;
+}
+
 // findClosestIntersection (tracer.cl:537-742), one loop per object type.  Loop
 // indices are wave-uniform, so object data arrives through scalar loads.
 template <int FL>
@@ -770,6 +807,24 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         h.pk = c ? pack_hit(P.slot, P.key) : h.pk;
     };
     int p = 0;
+    // Affine scenes: the leading planes whose row 1 is (+-0, m1, +-0, m3) -- floors and
+    // ceilings, S.n_planes_y of them in list order -- skip the +-0 terms (plane_rows_nz).
+    // (Dispatching every plane, or every run of planes, on its zero pattern measured
+    // slower: C2 +4-6 %.)
+    if constexpr (A) {
+        const int npy = (PTMI_ABLATE & 512) ? 0 : S.n_planes_y;  // DIAGNOSTIC 512: full rows for all
+        for (; p + 1 < npy; p += 2) {
+            const PlaneRec P0 = S.planes[p], P1 = S.planes[p + 1];
+            double oy0, dy0, oy1, dy1, q0, q1;
+            bool k0, k1;
+            plane_rows_nz<2>(P0.row1, ro, rd, oy0, dy0);
+            plane_rows_nz<2>(P1.row1, ro, rd, oy1, dy1);
+            plane_q(oy0, dy0, q0, k0);
+            plane_q(oy1, dy1, q1, k1);
+            plane_take(P0, q0, k0);
+            plane_take(P1, q1, k1);
+        }
+    }
     for (; p + 1 < np; p += 2) {
         const PlaneRec P0 = S.planes[p], P1 = S.planes[p + 1];
         double oy0, dy0, oy1, dy1, q0, q1;
@@ -980,27 +1035,26 @@ __device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__
 #endif
 }
 
-// group_walks' deferred verification for a walk done elsewhere (the walker wave):
-// h is the tentative winner over h0 (the primitives' best); a winning triangle
-// without certificate whose exact gate chain fails sends the ray to an eager re-walk.
-template <bool A>
-__device__ __forceinline__ void group_walks_finish(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes,
-                                                   d4 ro, d4 rd, Hit& h, const Hit& h0) {
-    if (h.tri < 0) return;
-    bool ok = true;
-    for (int j = S.run_end[3]; j < S.run_end[4]; j++) {  // uniform j: scalar loads of the winner's object
-        if (hit_obj(h) != j) continue;
-        const DevObject& ob = S.objs[j];
-        const d4 o = xpt<A>(ob.inv, ob.st, ro);
-        const d4 d = xdir<A>(ob.inv, ob.st, rd);
-        ok = chain_certified(S, h.chain, o, d, h.t) || verify_chain(S, h.chain, o, d);
+// Position of the r-th (0-based) set bit of m (r < popc(m)).
+__device__ __forceinline__ int nth_set_bit(unsigned long long m, int r) {
+    uint32_t w = (uint32_t)m;
+    int base = 0;
+    int pc = __popc(w);
+    if (r >= pc) {
+        r -= pc;
+        w = (uint32_t)(m >> 32);
+        base = 32;
     }
-    if (!ok) {
-        PTMI_COUNT(11);  // (stats build: eager re-walks)
-        h = h0;
-        bool cert = false;
-        group_walks_impl<A, true>(S, stk, lds_nodes, ro, rd, h, cert);
+#pragma unroll
+    for (int span = 16; span >= 1; span >>= 1) {
+        pc = __popc(w & ((1u << span) - 1u));
+        if (r >= pc) {
+            r -= pc;
+            w >>= span;
+            base += span;
+        }
     }
+    return base;
 }
 
 // schlick (tracer.cl:485-505)
@@ -1430,7 +1484,7 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
         __syncthreads();
     }
 #if PTMI_STATS
-    if ((threadIdx.x & 63) < 24) ptmi_wstat[threadIdx.x >> 6][threadIdx.x & 63] = 0;
+    if ((threadIdx.x & 63) < 32) ptmi_wstat[threadIdx.x >> 6][threadIdx.x & 63] = 0;
 #endif
     const int W = S.cam.width, H = S.cam.height;
     const int tiles_x = (W + kTile - 1) / kTile;
@@ -1439,18 +1493,51 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
     const int tile = blockIdx.x * (kBlock / 64) + wave;
     if (tile >= tiles_x * tiles_y) return;
     if ((uint32_t)tile % tile_stride != tile_offset) return;
-    const int px = (tile % tiles_x) * kTile + (lane & 7);
-    const int py = (tile / tiles_x) * kTile + (lane >> 3);
-    if (px >= W || py >= H) return;
+    const int px0 = (tile % tiles_x) * kTile + (lane & 7);
+    const int py0 = (tile / tiles_x) * kTile + (lane >> 3);
+    if (px0 >= W || py0 >= H) return;
     constexpr bool A = !(FL & F_PROJ);
-    const uint32_t i = (uint32_t)py * (uint32_t)W + (uint32_t)px;
+    const uint32_t i = (uint32_t)py0 * (uint32_t)W + (uint32_t)px0;
     const uint32_t c0 = s_begin + blockIdx.y * chunk_len;
     const uint32_t c1 = min(s_end, c0 + chunk_len);
     // fgi / fgi2 (tracer.cl:839-841): double division rounded to float.
     const double seed = seeds[i];
-    const float fgi = (float)(seed / (double)S.n_list);
-    const float fgi2 = (float)(seed / (double)samples);
-    double cr = 0.0, cg = 0.0, cb = 0.0;
+    // The lane's current segment: samples [n_gen .., c_end) of the pixel (px, py) whose
+    // sums are accumulated at acc_lds[owner].  It starts as the lane's own pixel and chunk;
+    // a lane that has finished takes the later half of the samples a busier lane has
+    // not started (see "Segment stealing" below).
+    int px = px0, py = py0, owner = lane;
+    float fgi = (float)(seed / (double)S.n_list);
+    float fgi2 = (float)(seed / (double)samples);
+    uint32_t c_end = c1;
+    double cr = 0.0, cg = 0.0, cb = 0.0;  // the current segment's sums
+    bool seg_open = true;                 // cr/cg/cb not yet added to acc_lds[owner]
+    // Per-pixel chunk sums of the wave's 64 pixels (lane-indexed, SoA) when stealing.
+    constexpr bool kSteal = PTMI_STEAL && (FL & F_GROUPS);
+    __shared__ double acc_lds[kSteal ? 3 * kBlock : 1];
+    double* acc = acc_lds + (threadIdx.x & ~63);
+    if constexpr (kSteal) {
+        acc[lane] = 0.0;
+        acc[64 + lane] = 0.0;
+        acc[128 + lane] = 0.0;
+    }
+    // Adds every finishing lane's segment sums into its owner's pixel sums, one lane at
+    // a time in lane order (two lanes may finish segments of the same pixel together):
+    // a fixed order, so the image is deterministic.
+    auto flush = [&](bool fin) {
+        unsigned long long m = __ballot(fin && seg_open);
+        while (m) {
+            const int k = __ffsll((long long)m) - 1;
+            if (lane == k) {
+                acc[owner] = acc[owner] + cr;
+                acc[64 + owner] = acc[64 + owner] + cg;
+                acc[128 + owner] = acc[128 + owner] + cb;
+                cr = cg = cb = 0.0;
+                seg_open = false;
+            }
+            m &= m - 1;
+        }
+    };
     // Camera rays are produced in wave-wide batches into a kCamDepth-deep per-lane
     // ring buffer (LDS) and consumed by path regeneration: generating them at the
     // moment each lane needs one would run the camera block (2 noise3D + the
@@ -1477,11 +1564,46 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
     Hit hp;
     PTMI_TSTAMP(t_loop);
     for (;;) {
-        if (!__any(active || nb > 0 || n_gen < c1)) break;
+        if (!__any(active || nb > 0 || n_gen < c_end)) break;
         PTMI_TSTAMP(t_a);
-        const bool need = nb < kCamDepth && n_gen < c1;
+        if constexpr (kSteal) {
+        // Segment stealing.  Lanes whose pixels need long paths (a mesh in view) keep
+        // a wave busy while the others have finished their chunk; each finished lane
+        // takes the later half of the samples a busy lane has not started.  The sum of
+        // a pixel's samples is then a sum of segment sums (like the chunk sums), in an
+        // order fixed by the wave's own execution.
+        if (S.steal) {
+            const bool fin = !active && nb == 0 && n_gen >= c_end;
+            const unsigned long long F = __ballot(fin);
+            if (F) {
+                flush(fin);
+                const uint32_t rem = n_gen < c_end ? c_end - n_gen : 0u;  // samples not yet started
+                const unsigned long long V = __ballot(rem >= kStealMin);
+                const int nt = min(__popcll(F), __popcll(V));
+                if (nt > 0) {
+                    const unsigned long long below = (1ull << lane) - 1ull;
+                    const int rf = __popcll(F & below), rv = __popcll(V & below);
+                    const bool thief = fin && rf < nt;
+                    const bool victim = !fin && rem >= kStealMin && rv < nt;
+                    const int src = thief ? nth_set_bit(V, rf) : lane;
+                    const int vx = __shfl(px, src), vy = __shfl(py, src), vo = __shfl(owner, src);
+                    const float vf = __shfl(fgi, src), vf2 = __shfl(fgi2, src);
+                    const uint32_t vg = (uint32_t)__shfl((int)n_gen, src), ve = (uint32_t)__shfl((int)c_end, src);
+                    const uint32_t mid = vg + ((ve - vg) - (ve - vg) / 2u);  // the victim keeps the larger half
+                    if (thief) {
+                        px = vx, py = vy, owner = vo, fgi = vf, fgi2 = vf2;
+                        n_gen = mid;
+                        c_end = ve;
+                        seg_open = true;
+                    }
+                    if (victim) c_end = mid;
+                }
+            }
+        }
+        }
+        const bool need = nb < kCamDepth && n_gen < c_end;
         const int n_need = __popcll(__ballot(need));
-        const int n_starve = __popcll(__ballot(nb == 0 && !active && n_gen < c1));
+        const int n_starve = __popcll(__ballot(nb == 0 && !active && n_gen < c_end));
         constexpr int kRefillStarve = (FL & F_GROUPS) ? PTMI_REFILL_STARVE_GROUPS : PTMI_REFILL_STARVE;
         if (n_need >= kRefillNeed || n_starve >= kRefillStarve || (n_starve > 0 && !__any(active))) {
             if (need) {
@@ -1530,6 +1652,9 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
         Hit h;
 #if PTMI_STATS
         PTMI_WADD(10, 1ull);
+        PTMI_WADD(26, (unsigned long long)__popcll(__ballot(!active && (nb > 0 || n_gen < c_end))));
+        PTMI_WADD(27, (unsigned long long)__popcll(__ballot(!active && nb == 0 && n_gen >= c_end)));
+        PTMI_WADD(28, (unsigned long long)__popcll(__ballot(active && !pending)));
 #endif
         if (active && !pending) {
             if (P.dead) {
@@ -1561,6 +1686,8 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
             }
         }
         PTMI_TADD(14, t_c);
+        PTMI_WADD(24, (unsigned long long)__popcll(__ballot(ready)));
+        PTMI_WADD(25, (unsigned long long)__popcll(__ballot(pending)));
         PTMI_TSTAMP(t_d);
         if (ready && bounce_shade<FL>(S, P, h, fgi, n_cur)) {
             cr = cr + P.ar;  // colors += accumColor (tracer.cl:1179)
@@ -1573,477 +1700,21 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
     PTMI_TADD(16, t_loop);
 #if PTMI_STATS
     if (PTMI_FIRST_ACTIVE())
-        for (int k = 0; k < 24; k++)
+        for (int k = 0; k < 32; k++)
             if (ptmi_wstat[threadIdx.x >> 6][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[threadIdx.x >> 6][k]);
 #endif
     double* o = out + ((size_t)blockIdx.y * ((size_t)W * H) + i) * 4;
-    o[0] = cr;
-    o[1] = cg;
-    o[2] = cb;
-    o[3] = (double)(c1 > c0 ? c1 - c0 : 0);
-}
-
-// ---- Walker waves (scenes with BVH groups) ---------------------------------------
-// A workgroup is kTracers tracer waves plus one walker wave.  Tracer waves run the
-// path loop of trace_kernel (one 8x8 tile x sample chunk each) but never walk a BVH:
-// a lane whose ray needs a walk (group_needs_walk) posts it to the workgroup's
-// request pool in LDS and parks; the walker wave walks the pool's rays with all its
-// lanes, taking a new ray into a lane as soon as that lane's walk ends, and posts
-// each certified closest hit back.  Walks so run with full lanes instead of a
-// wave's ~20 parked rays at the pace of its longest walk, and a tracer keeps tracing
-// its other lanes meanwhile.  No wave ever waits for a result it produces itself:
-// walkers wait for nothing but requests (they sleep when the pool is empty and leave
-// once every tracer has left); tracers wait only for their posted walks.
-// Per request (one slot per tracer lane): the world ray and the primitives' best
-// (t, pk); per result: t, u, v, pk, tri.  The candidate set and the winner are those
-// of group_walks (same walk, same deferred gate verification), so images are
-// identical.  A watchdog bounds both loops (a fault, never a hang).
-#ifndef PTMI_WW_TRACERS
-#define PTMI_WW_TRACERS 3
-#endif
-#ifndef PTMI_WW_STEPS
-#define PTMI_WW_STEPS 1  // walk steps per walker iteration (more amortise the take / start / post stages)
-#endif
-#ifndef PTMI_WW_REFILL
-#define PTMI_WW_REFILL 8  // a walker takes new requests once this many of its lanes are idle
-#endif
-static constexpr int kTracers = PTMI_WW_TRACERS;
-static constexpr int kWwBlock = (kTracers + 1) * 64;
-static constexpr int kReqSlots = kTracers * 64;
-static constexpr int kWalkDone = INT32_MIN + 1;  // walk cursor past the last stack entry
-static constexpr uint32_t kWatchdog = 1u << 26;  // loop iterations per wave before the watchdog fires
-__device__ int ptmi_watchdog_fired;
-
-template <bool A>
-struct WwShared {
-    unsigned long long pend[kTracers];  // request bits of tracer wave w (set by it, cleared by the walker)
-    int finished;                       // tracer waves that have left their loop
-    int done[kReqSlots];                // 1: result posted (walker -> tracer)
-    double req[A ? 7 : 9][kReqSlots];   // ro.xyz, rd.xyz, primitives' best t (+ ro.w, rd.w)
-    int req_pk[kReqSlots];
-    double res[3][kReqSlots];  // t, u, v
-    int res_pk[kReqSlots], res_tri[kReqSlots];
-};
-
-__device__ __forceinline__ void ww_fence_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
-__device__ __forceinline__ void ww_fence_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); }
-
-// Position of the r-th (0-based) set bit of m (r < popc(m)).
-__device__ __forceinline__ int nth_set_bit(unsigned long long m, int r) {
-    uint32_t w = (uint32_t)m;
-    int base = 0;
-    int pc = __popc(w);
-    if (r >= pc) {
-        r -= pc;
-        w = (uint32_t)(m >> 32);
-        base = 32;
-    }
-#pragma unroll
-    for (int span = 16; span >= 1; span >>= 1) {
-        pc = __popc(w & ((1u << span) - 1u));
-        if (r >= pc) {
-            r -= pc;
-            w >>= span;
-            base += span;
-        }
-    }
-    return base;
-}
-// The lowest k set bits of m.
-__device__ __forceinline__ unsigned long long lowest_set_bits(unsigned long long m, int k) {
-    unsigned long long rest = m;
-    for (int i = 0; i < k; i++) rest &= rest - 1;
-    return m ^ rest;
-}
-
-// The walker wave of a workgroup (see above).
-template <int FL>
-__device__ __forceinline__ void ww_walker(const DevScene& S, WwShared<!(FL & F_PROJ)>& sh, int* __restrict__ stk,
-                                          const Node4* lds_nodes) {
-    constexpr bool A = !(FL & F_PROJ);
-    const int lane = threadIdx.x & 63;
-    const int g0 = S.run_end[3], g1 = S.run_end[4];
-    bool has = false, setup = false;
-    int slot = 0, wj = 0, wkey = 0, cur = kWalkDone, sp = 0, vchain = -1;
-    d4 wro = mk(0, 0, 0, 1), wrd = mk(0, 0, 0, 0), o = wro, d = wrd;
-    Hit h{1024.0, -1, -1, -1, 0.0, 0.0};
-    float of[3] = {0, 0, 0}, rf[3] = {0, 0, 0}, ofr[3] = {0, 0, 0}, dt[3] = {0, 0, 0};
-#if PTMI_STATS
-    // [24] walker iterations [25] lanes walking per iteration (sum) [26] walker cycles
-    // [27] cycles in take/start/post [28] walks posted [29] iterations with the pool empty
-    unsigned long long ws_it = 0, ws_lanes = 0, ws_cyc_admin = 0, ws_posted = 0, ws_empty = 0;
-    const unsigned long long ws_t0 = clock64();
-    auto ws_flush = [&]() {
-        if (lane == 0) {
-            atomicAdd(&ptmi_stats[24], ws_it);
-            atomicAdd(&ptmi_stats[25], ws_lanes);
-            atomicAdd(&ptmi_stats[26], clock64() - ws_t0);
-            atomicAdd(&ptmi_stats[27], ws_cyc_admin);
-            atomicAdd(&ptmi_stats[28], ws_posted);
-            atomicAdd(&ptmi_stats[29], ws_empty);
-        }
-    };
-#define WS(x) x
-#else
-#define WS(x)
-#endif
-    for (uint32_t it = 0;; it++) {
-        if (it >= kWatchdog) {
-            if (lane == 0) atomicExch(&ptmi_watchdog_fired, 1);
-            WS(ws_flush());
-            return;
-        }
-        WS(ws_it++;)
-        WS(const unsigned long long ws_a = clock64();)
-        // 1. Take requests into idle lanes: the k-th idle lane takes the k-th pending slot.
-        const int n_idle = __popcll(__ballot(!has));
-        if (n_idle >= PTMI_WW_REFILL || n_idle == 64) {
-            unsigned long long m[kTracers];
-            int total = 0;
-#pragma unroll
-            for (int w = 0; w < kTracers; w++) {
-                m[w] = __hip_atomic_load(&sh.pend[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                total += __popcll(m[w]);
-            }
-            ww_fence_acquire();
-            if (total == 0 && n_idle == 64) {
-                if (__hip_atomic_load(&sh.finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == kTracers) {
-                    WS(ws_flush());
-                    return;  // every tracer has left: no request can come
-                }
-                WS(ws_empty++;)
-                __builtin_amdgcn_s_sleep(2);
-                continue;
-            }
-            const int take = min(n_idle, total);
-            if (take > 0) {
-                if (lane == __ffsll((long long)__ballot(1)) - 1) {  // one lane clears the taken bits
-                    int before = 0;
-#pragma unroll
-                    for (int w = 0; w < kTracers; w++) {
-                        const int c = min(max(take - before, 0), __popcll(m[w]));
-                        if (c > 0)
-                            __hip_atomic_fetch_and(&sh.pend[w], ~lowest_set_bits(m[w], c), __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-                        before += __popcll(m[w]);
-                    }
-                }
-                const int rank = __popcll(__ballot(!has) & ((1ull << lane) - 1ull));
-                if (!has && rank < take) {
-                    int r = rank, w = 0;
-#pragma unroll
-                    for (int k = 0; k < kTracers - 1; k++) {
-                        const int pc = __popcll(m[w]);
-                        if (r >= pc) {
-                            r -= pc;
-                            w++;
-                        }
-                    }
-                    slot = w * 64 + nth_set_bit(m[w], r);
-                    wro = mk(sh.req[0][slot], sh.req[1][slot], sh.req[2][slot], A ? 1.0 : sh.req[7][slot]);
-                    wrd = mk(sh.req[3][slot], sh.req[4][slot], sh.req[5][slot], A ? 0.0 : sh.req[8][slot]);
-                    h = Hit{sh.req[6][slot], sh.req_pk[slot], -1, -1, 0.0, 0.0};
-                    has = true;
-                    setup = true;
-                    wj = g0;
-                }
-            }
-        }
-        // 2. Start the walk of object wj (culling whole objects by their hull); a lane
-        //    past the last group object has its closest hit: certify it and post it.
-        for (int j = g0; j < g1; j++) {  // uniform j: the object's data arrives by scalar loads
-            if (!(setup && wj == j)) continue;
-            const DevObject& ob = S.objs[j];
-            o = xpt<A>(ob.inv, ob.st, wro);
-            d = xdir<A>(ob.inv, ob.st, wrd);
-            const d4 r = mk(rcp_walk(d.x), rcp_walk(d.y), rcp_walk(d.z), 0.0);
-            const RootRec& R = S.root_rec[ob.child_base];  // one traversal index per group object
-            double tn;
-            if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1], R.hull_mx[2],
-                         h.t + prune_margin(h.t), tn)) {
-                wj = j + 1;
-                continue;
-            }
-            // walk_index's FP32 ray setup (same bound)
-            const double oo[3] = {o.x, o.y, o.z}, rr[3] = {r.x, r.y, r.z};
-            float omax = 0.0f;
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-                of[a] = (float)oo[a];
-                const float rv = (float)rr[a];
-                rf[a] = fminf(fmaxf(rv, -1e30f), 1e30f);
-                ofr[a] = of[a] * rf[a];
-                omax = fmaxf(omax, fabsf(of[a]));
-            }
-            const float E = 0x1p-21f * (R.bmax + 2.0f * omax) + 0x1p-120f;
-#pragma unroll
-            for (int a = 0; a < 3; a++) dt[a] = E * fabsf(rf[a]);
-            cur = R.entry;
-            sp = 0;
-            vchain = -1;
-            wkey = ob.key;
-            setup = false;
-        }
-        if (has && setup && wj >= g1) {
-            group_walks_finish<A>(S, stk, lds_nodes, wro, wrd, h, Hit{sh.req[6][slot], sh.req_pk[slot], -1, -1, 0.0, 0.0});
-            sh.res[0][slot] = h.t;
-            sh.res[1][slot] = h.u;
-            sh.res[2][slot] = h.v;
-            sh.res_pk[slot] = h.pk;
-            sh.res_tri[slot] = h.tri;
-            ww_fence_release();
-            __hip_atomic_store(&sh.done[slot], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            has = false;
-            setup = false;
-            WS(if (lane == __ffsll((long long)__ballot(1)) - 1) ws_posted += __popcll(__ballot(1));)
-        }
-        WS(ws_cyc_admin += clock64() - ws_a;)
-        WS(ws_lanes += __popcll(__ballot(has && !setup));)
-        // 3. Steps of every walk in progress (walk_index's loop body), up to
-        //    PTMI_WW_STEPS per iteration while most walking lanes keep walking.
-        const int n_walk0 = __popcll(__ballot(has && !setup));
-        for (int stp = 0; stp < PTMI_WW_STEPS; stp++) {
-        if (stp > 0 && __popcll(__ballot(has && !setup)) * 4 < n_walk0 * 3) break;
-        if (has && !setup) {
-            bool pop = true;
-            if (cur >= 0) {
-                const float4* src = cur < kLdsNodes ? reinterpret_cast<const float4*>(lds_nodes) + 7 * cur
-                                                    : reinterpret_cast<const float4*>(S.nodes4) + 7 * cur;
-                float4 q[7];
-#pragma unroll
-                for (int u = 0; u < 7; u++) q[u] = src[u];
-                const float mnx[4] = {q[0].x, q[0].y, q[0].z, q[0].w}, mny[4] = {q[1].x, q[1].y, q[1].z, q[1].w};
-                const float mnz[4] = {q[2].x, q[2].y, q[2].z, q[2].w}, mxx[4] = {q[3].x, q[3].y, q[3].z, q[3].w};
-                const float mxy[4] = {q[4].x, q[4].y, q[4].z, q[4].w}, mxz[4] = {q[5].x, q[5].y, q[5].z, q[5].w};
-                const int ch[4] = {__float_as_int(q[6].x), __float_as_int(q[6].y), __float_as_int(q[6].z),
-                                   __float_as_int(q[6].w)};
-                const double limd = h.t + prune_margin(h.t);
-                const float lim = (float)limd * (1.0f + 0x1p-22f) + 0x1p-100f;  // >= limd
-                float k[4];
-                int c[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    c[i] = ch[i];
-                    const float ax = fmaf(mnx[i], rf[0], -ofr[0]), bx = fmaf(mxx[i], rf[0], -ofr[0]);
-                    const float ay = fmaf(mny[i], rf[1], -ofr[1]), by = fmaf(mxy[i], rf[1], -ofr[1]);
-                    const float az = fmaf(mnz[i], rf[2], -ofr[2]), bz = fmaf(mxz[i], rf[2], -ofr[2]);
-                    const float tn = fmaxf(fmaxf(fminf(ax, bx) - dt[0], fminf(ay, by) - dt[1]), fminf(az, bz) - dt[2]);
-                    const float tf = fminf(fminf(fmaxf(ax, bx) + dt[0], fmaxf(ay, by) + dt[1]), fmaxf(az, bz) + dt[2]);
-                    const bool cull = tn > tf || tn > lim || tf < 0.0f || c[i] == kEmptyChild;
-                    k[i] = cull ? __builtin_huge_valf() : fmaxf(tn, -__builtin_huge_valf());  // NaN -> -inf
-                }
-#define PTMI_CX(a, b)                                      \
-    if (k[b] < k[a]) {                                     \
-        const float tk = k[a];                             \
-        k[a] = k[b];                                       \
-        k[b] = tk;                                         \
-        const int tc = c[a];                               \
-        c[a] = c[b];                                       \
-        c[b] = tc;                                         \
-    }
-                PTMI_CX(0, 1) PTMI_CX(2, 3) PTMI_CX(0, 2) PTMI_CX(1, 3) PTMI_CX(1, 2)
-#undef PTMI_CX
-                if (k[3] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[3];
-                if (k[2] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[2];
-                if (k[1] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[1];
-                if (k[0] < __builtin_huge_valf()) {
-                    cur = c[0];
-                    pop = false;
-                }
-            } else if (cur != kEmptyChild && cur != kWalkDone) {
-                const int code = -cur - 1;
-                const int first = code >> 3, end = first + (code & 7);
-                for (int i = first; i < end; i++) tri_test<false>(S, S.tris[i], o, d, wj, wkey, h, vchain);
-            }
-            if (pop) {
-                if (sp == 0) {
-                    wj++;  // this object's walk is over: the next object (or the post) in stage 2
-                    setup = true;
-                } else {
-                    cur = stk[(--sp) * kStkStride];
-                }
-            }
-        }
-        }
-    }
-}
-
-template <int FL>
-__global__ __launch_bounds__(kWwBlock) void trace_kernel_ww(DevScene S, uint32_t samples, uint32_t s_begin,
-                                                            uint32_t s_end, uint32_t chunk_len, uint32_t tile_stride,
-                                                            uint32_t tile_offset, const double* __restrict__ seeds,
-                                                            const double* __restrict__ sunf,
-                                                            double* __restrict__ out) {
-    constexpr bool A = !(FL & F_PROJ);
-    static_assert((FL & F_GROUPS) != 0, "walker waves serve BVH scenes");
-    __shared__ float4 node_lds4[(kLdsNodes > 0 ? kLdsNodes : 1) * 7];
-    __shared__ WwShared<A> sh;
-    const Node4* node_lds = reinterpret_cast<const Node4*>(node_lds4);
-    {
-        const int nl = min(kLdsNodes, S.n_nodes4) * 7;
-        const float4* src = reinterpret_cast<const float4*>(S.nodes4);
-        for (int k = threadIdx.x; k < nl; k += kWwBlock) node_lds4[k] = src[k];
-        if (threadIdx.x < kTracers) sh.pend[threadIdx.x] = 0ull;
-        if (threadIdx.x == 0) sh.finished = 0;
-        for (int k = threadIdx.x; k < kReqSlots; k += kWwBlock) sh.done[k] = 0;
-        __syncthreads();
-    }
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // Walker: the last wave.  Its traversal stack (per lane, lane-interleaved) in LDS.
-    __shared__ int stk_lds[kStack * kStkStride];
-    if (wave == kTracers) {
-        ww_walker<FL>(S, sh, stk_lds + lane, node_lds);
-        return;
-    }
-    const int W = S.cam.width, H = S.cam.height;
-    const int tiles_x = (W + kTile - 1) / kTile;
-    const int tiles_y = (H + kTile - 1) / kTile;
-    const int tile = blockIdx.x * kTracers + wave;
-    const int px = (tile % tiles_x) * kTile + (lane & 7);
-    const int py = (tile / tiles_x) * kTile + (lane >> 3);
-    // No early exit: every tracer wave reaches the `finished` count at the end.
-    const bool valid = tile < tiles_x * tiles_y && (uint32_t)tile % tile_stride == tile_offset && px < W && py < H;
-    const uint32_t i = valid ? (uint32_t)py * (uint32_t)W + (uint32_t)px : 0u;
-    const uint32_t c0 = s_begin + blockIdx.y * chunk_len;
-    const uint32_t c1 = valid ? min(s_end, c0 + chunk_len) : c0;
-    const double seed = valid ? seeds[i] : 0.0;
-    const float fgi = (float)(seed / (double)S.n_list);
-    const float fgi2 = (float)(seed / (double)samples);
-    double cr = 0.0, cg = 0.0, cb = 0.0;
-    constexpr int kCamComp = A ? 6 : 8;
-    __shared__ double cam_lds[kTracers * kCamComp * 64];
-    double* cam_wave = cam_lds + wave * (kCamComp * 64) + lane;
-    const int rslot = wave * 64 + lane;  // this lane's request slot
-    uint32_t n_gen = c0, n_cur = 0;
-    int nb = 0;
-    bool active = false, pending = false;
-    PathState P;
-#if PTMI_STATS
-    // [30] tracer iterations [31] pending lanes per iteration (sum) [32] ready lanes per
-    // iteration (sum) [33] tracer cycles [34] iterations without a ready lane
-    unsigned long long ts_it = 0, ts_pend = 0, ts_ready = 0, ts_idle = 0;
-    const unsigned long long ts_t0 = clock64();
-#endif
-    for (uint32_t it = 0;; it++) {
-        if (!__any(active || nb > 0 || n_gen < c1)) break;
-#if PTMI_STATS
-        ts_it++;
-#endif
-        if (it >= kWatchdog) {
-            if (lane == 0) atomicExch(&ptmi_watchdog_fired, 1);
-            cr = cg = cb = __builtin_nan("");
-            break;
-        }
-        // Camera rays in wave-wide batches (as trace_kernel; one buffered ray per lane).
-        const bool need = nb == 0 && n_gen < c1;
-        const int n_need = __popcll(__ballot(need));
-        const int n_starve = __popcll(__ballot(nb == 0 && !active && n_gen < c1));
-        if (n_need >= kRefillNeed || n_starve >= PTMI_REFILL_STARVE_GROUPS || (n_starve > 0 && !__any(active))) {
-            if (need) {
-                d4 ro, rd;
-                ray_for_pixel<(FL & F_DOF) != 0, A>(S.cam, sunf, (unsigned)px, (unsigned)py,
-                                                    noise3d(fgi, (float)n_gen, fgi2), noise3d(fgi, fgi2, (float)n_gen),
-                                                    (int)n_gen, ro, rd);
-                cam_wave[0 * 64] = ro.x;
-                cam_wave[1 * 64] = ro.y;
-                cam_wave[2 * 64] = ro.z;
-                cam_wave[3 * 64] = rd.x;
-                cam_wave[4 * 64] = rd.y;
-                cam_wave[5 * 64] = rd.z;
-                if constexpr (!A) {
-                    cam_wave[6 * 64] = ro.w;
-                    cam_wave[7 * 64] = rd.w;
-                }
-                n_gen++;
-                nb = 1;
-            }
-        }
-        if (!active && nb > 0) {
-            const d4 cro = mk(cam_wave[0 * 64], cam_wave[1 * 64], cam_wave[2 * 64], A ? 1.0 : cam_wave[6 * 64]);
-            const d4 crd = mk(cam_wave[3 * 64], cam_wave[4 * 64], cam_wave[5 * 64], A ? 0.0 : cam_wave[7 * 64]);
-            start_path<A, (FL & F_DOF) != 0>(P, cro, crd);
-            n_cur = n_gen - 1u;
-            nb = 0;
-            active = true;
-        }
-        bool ready = false, posting = false;
-        Hit h;
-        if (pending) {  // a posted walk came back
-            if (__hip_atomic_load(&sh.done[rslot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                ww_fence_acquire();
-                h.t = sh.res[0][rslot];
-                h.u = sh.res[1][rslot];
-                h.v = sh.res[2][rslot];
-                h.pk = sh.res_pk[rslot];
-                h.tri = sh.res_tri[rslot];
-                h.chain = -1;
-                sh.done[rslot] = 0;
-                pending = false;
-                ready = true;
-            }
-        } else if (active) {
-            if (P.dead) {
-                h.pk = -1;
-                ready = true;
-            } else {
-                h = find_closest_prims<FL>(S, P.ro, P.rd);
-                if (group_needs_walk<A>(S, P.ro, P.rd, h)) {
-                    sh.req[0][rslot] = P.ro.x;
-                    sh.req[1][rslot] = P.ro.y;
-                    sh.req[2][rslot] = P.ro.z;
-                    sh.req[3][rslot] = P.rd.x;
-                    sh.req[4][rslot] = P.rd.y;
-                    sh.req[5][rslot] = P.rd.z;
-                    sh.req[6][rslot] = h.t;
-                    if constexpr (!A) {
-                        sh.req[7][rslot] = P.ro.w;
-                        sh.req[8][rslot] = P.rd.w;
-                    }
-                    sh.req_pk[rslot] = h.pk;
-                    pending = true;
-                    posting = true;
-                } else {
-                    ready = true;
-                }
-            }
-        }
-        // Publish this iteration's requests: their data first, then one atomic OR of the
-        // wave's new bits (the walker reads a slot only after it sees its bit).
-        const unsigned long long fresh = __ballot(posting);
-        if (fresh) {
-            ww_fence_release();
-            if (lane == 0) __hip_atomic_fetch_or(&sh.pend[wave], fresh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-#if PTMI_STATS
-        ts_pend += __popcll(__ballot(pending));
-        ts_ready += __popcll(__ballot(ready));
-        ts_idle += __any(ready) ? 0 : 1;
-#endif
-        if (!__any(ready)) __builtin_amdgcn_s_sleep(1);  // every path waits for its walk
-        if (ready && bounce_shade<FL>(S, P, h, fgi, n_cur)) {
-            cr = cr + P.ar;  // colors += accumColor (tracer.cl:1179)
-            cg = cg + P.ag;
-            cb = cb + P.ab;
-            active = false;
-        }
-    }
-    if (valid) {
-        double* o = out + ((size_t)blockIdx.y * ((size_t)W * H) + i) * 4;
+    if constexpr (kSteal) {
+        flush(true);
+        o[0] = acc[lane];
+        o[1] = acc[64 + lane];
+        o[2] = acc[128 + lane];
+    } else {
         o[0] = cr;
         o[1] = cg;
         o[2] = cb;
-        o[3] = (double)(c1 > c0 ? c1 - c0 : 0);
     }
-#if PTMI_STATS
-    if (lane == 0) {
-        atomicAdd(&ptmi_stats[30], ts_it);
-        atomicAdd(&ptmi_stats[31], ts_pend);
-        atomicAdd(&ptmi_stats[32], ts_ready);
-        atomicAdd(&ptmi_stats[33], clock64() - ts_t0);
-        atomicAdd(&ptmi_stats[34], ts_idle);
-    }
-#endif
-    if (lane == 0) __hip_atomic_fetch_add(&sh.finished, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    o[3] = (double)(c1 > c0 ? c1 - c0 : 0);
 }
 
 // DoF aperture offsets sunflower(S, 2, n) for n in [0, S) (tracer.cl:221-248,
@@ -2153,35 +1824,10 @@ __global__ __launch_bounds__(256) void seeds_kernel(double* __restrict__ seeds, 
 }
 
 // ---- host-side launch wrappers (called from ptmi_api.cpp) ----------------------
-// flags: the F_* feature bits, plus kFlagNoWalker (host only): BVH scenes on
-// trace_kernel's in-wave walks instead of walker waves (A/B measurement, tests).
-static constexpr int kFlagNoWalker = 64;
-static bool use_walker(int flags) { return (flags & F_GROUPS) && !(flags & kFlagNoWalker); }
-int trace_block_threads(int flags) { return use_walker(flags) ? kWwBlock : kBlock; }
-int trace_tiles_per_block(int flags) { return use_walker(flags) ? kTracers : kBlock / 64; }
-
-int watchdog_fired(bool clear) {
-    int v = 0;
-    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(ptmi_watchdog_fired), sizeof(int)) != hipSuccess) return -1;
-    if (v && clear) {
-        const int z = 0;
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(ptmi_watchdog_fired), &z, sizeof(int));
-    }
-    return v;
-}
+int trace_block_threads(int flags) { return kBlock; }
+int trace_tiles_per_block(int flags) { return kBlock / 64; }
 
 const void* trace_kernel_symbol(int flags) {
-    if (use_walker(flags)) {
-        if (flags & F_TEX) return reinterpret_cast<const void*>(&trace_kernel_ww<F_ALL | F_PROJ | F_TEX>);
-        if (flags & F_PROJ) return reinterpret_cast<const void*>(&trace_kernel_ww<F_ALL | F_PROJ>);
-        switch (flags & F_ALL) {
-#define K(f) \
-    case f: return reinterpret_cast<const void*>(&trace_kernel_ww<f>);
-            K(1) K(3) K(5) K(7) K(9) K(11) K(13) K(15)
-#undef K
-        }
-        return nullptr;
-    }
     if (flags & F_TEX) return reinterpret_cast<const void*>(&trace_kernel<F_ALL | F_PROJ | F_TEX>);
     if (flags & F_PROJ) return reinterpret_cast<const void*>(&trace_kernel<F_ALL | F_PROJ>);
     switch (flags & F_ALL) {
@@ -2197,29 +1843,6 @@ hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, uint32_t
                         uint32_t chunk_len, uint32_t nchunks, uint32_t tile_stride, uint32_t tile_offset,
                         const double* seeds, const double* sunf, double* out, hipStream_t st) {
     const int tiles = ((S.cam.width + kTile - 1) / kTile) * ((S.cam.height + kTile - 1) / kTile);
-    if (use_walker(flags)) {  // BVH scene: kTracers tracer waves + one walker wave per workgroup
-        const dim3 gw((tiles + kTracers - 1) / kTracers, nchunks);
-#define KW(f) hipLaunchKernelGGL(trace_kernel_ww<f>, gw, dim3(kWwBlock), 0, st, S, samples, s_begin, s_end, chunk_len, \
-                                 tile_stride, tile_offset, seeds, sunf, out)
-        if (flags & F_TEX) {
-            KW(F_ALL | F_PROJ | F_TEX);
-        } else if (flags & F_PROJ) {
-            KW(F_ALL | F_PROJ);
-        } else {
-            switch (flags & F_ALL) {
-            case 1: KW(1); break;
-            case 3: KW(3); break;
-            case 5: KW(5); break;
-            case 7: KW(7); break;
-            case 9: KW(9); break;
-            case 11: KW(11); break;
-            case 13: KW(13); break;
-            case 15: KW(15); break;
-            }
-        }
-#undef KW
-        return hipGetLastError();
-    }
     constexpr int wpb = kBlock / 64;
     const dim3 grid((tiles + wpb - 1) / wpb, nchunks);
     if (flags & F_TEX) {  // textured scene: the generic instantiation plus the texture lookups

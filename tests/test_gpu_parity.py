@@ -82,7 +82,10 @@ def test_hip_matches_live_reference(scene, w, h, spp, ap, fl, seed):
 def test_generic_instantiation_matches(monkeypatch, scene, ap, force):
     """The feature-specialised kernel instantiation and the generic ones give
     identical images: 15 = all features compiled in (affine), 31 = all features
-    with the literal double4 w-lane arithmetic (the path for non-affine scenes)."""
+    with the literal double4 w-lane arithmetic (the path for non-affine scenes).
+    Segment stealing off: with it, a pixel's sum is a sum of segment sums whose
+    boundaries follow each instantiation's own wave schedule."""
+    monkeypatch.setenv("PTMI_NO_STEAL", "1")
     w, h, spp = 40, 24, 3
     objs, tris, grps, cam = scene_inputs(scene, w, h, ap, 1.6 if ap else 0.0)
     seeds = layout.seeds_go_float64(w * h, 77)
@@ -96,7 +99,9 @@ def test_generic_instantiation_matches(monkeypatch, scene, ap, force):
 def test_affine_cores_match_generic_large(monkeypatch, scene, ap):
     """The affine instantiations' divide / sqrt / rsqrt cores (csrc/ptmi_fp64core.h)
     against the generic instantiation's full compiler expansions over a larger
-    frame: 160x120 at 24 spp (~1.8 M paths), images bit-identical."""
+    frame: 160x120 at 24 spp (~1.8 M paths), images bit-identical (segment stealing
+    off, as in test_generic_instantiation_matches)."""
+    monkeypatch.setenv("PTMI_NO_STEAL", "1")
     w, h, spp = 160, 120, 24
     objs, tris, grps, cam = scene_inputs(scene, w, h, ap, 1.6 if ap else 0.0)
     seeds = layout.seeds_go_float64(w * h, 91)
@@ -282,15 +287,19 @@ def test_trace_multi_matches_single_device(scene, w, h, spp, split, ndev):
     assert all(timing[k] >= 0 for k in timing) and timing["total_ms"] >= timing["render_ms"]
 
 
-@pytest.mark.parametrize("scene,w,h,spp,ap", [("teapot", 96, 64, 5, 0.0), ("gopher", 80, 64, 4, 0.0),
-                                              ("teapot", 64, 48, 3, 0.15), ("christian", 64, 48, 3, 0.0),
-                                              ("transparent_teapot", 64, 48, 4, 0.0)])
-def test_walker_waves_match_in_wave_walks(monkeypatch, scene, w, h, spp, ap):
-    """BVH scenes: the walker-wave kernel (trace_kernel_ww, PTMI_WALKER=1) and
-    trace_kernel's in-wave walks (the default) give bit-identical images."""
-    objs, tris, grps, cam = scene_inputs(scene, w, h, ap, 1.6 if ap else 0.0)
-    seeds = layout.seeds_go_float64(w * h, 404)
-    inwave = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
-    monkeypatch.setenv("PTMI_WALKER", "1")
-    ww = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
-    assert np.array_equal(ww, inwave)
+@pytest.mark.parametrize("scene,w,h,spp", [("teapot", 96, 64, 40), ("gopher", 80, 64, 40),
+                                           ("transparent_teapot", 64, 48, 24)])
+def test_segment_stealing_matches_per_lane_order(monkeypatch, scene, w, h, spp):
+    """BVH scenes: finished lanes take over samples of busy lanes (trace_kernel's
+    segment stealing).  Every path is the same; only the grouping of a pixel's
+    sample sums changes, so the image equals the per-lane order (PTMI_NO_STEAL=1)
+    to FP64 summation rounding, and repeated runs are bit-identical."""
+    objs, tris, grps, cam = scene_inputs(scene, w, h)
+    seeds = layout.seeds_go_float64(w * h, 313)
+    a = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    b = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    monkeypatch.setenv("PTMI_NO_STEAL", "1")
+    c = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    assert np.array_equal(a, b)
+    assert np.abs(a - c).max() < 1e-13
+    assert not np.array_equal(a, c)  # stealing did regroup some sums

@@ -27,9 +27,8 @@ names = ["walks", "node4", "leaves", "tri_tests", "verifies", "gate_rejects", "o
          "walk_phases", "lanes_in_phases", "wave_iterations", "eager_rewalks",
          "cyc_refill", "cyc_prims_gate", "cyc_walk_phases", "cyc_shade", "cyc_loop", "exact_chain_verifies",
          "cyc_walk_loops", "walk_loop_wave_iters", "walks_no_leaf", "walks_root_only", "walks_improving", "x23",
-         "ww_walker_iters", "ww_walker_lanes", "ww_walker_cycles", "ww_walker_admin_cycles", "ww_walks_posted",
-         "ww_walker_empty_iters", "ww_tracer_iters", "ww_tracer_pending", "ww_tracer_ready", "ww_tracer_cycles",
-         "ww_tracer_idle_iters"]
+         "lanes_ready", "lanes_pending", "lanes_starving", "lanes_finished", "lanes_prims", "cyc_walk_node",
+         "cyc_walk_leaf", "walk_leaf_sections"]
 v = dict(zip(names, buf))
 n = W * H * spp
 print(scene, "spp", spp)
@@ -47,14 +46,11 @@ print("  walk-loop cycles per phase %.0f, loop iterations per phase %.1f, cycles
     v["cyc_walk_loops"] / max(v["walk_loop_wave_iters"], 1)))
 print("  camera/prims/shade cycles per non-walk wave iteration %.0f" % (
     (v["cyc_refill"] + v["cyc_prims_gate"] + v["cyc_shade"]) / max(v["wave_iterations"], 1)))
-if v["ww_walker_iters"]:
-    print("  walker: lanes walking per iteration %.1f, admin share of walker cycles %.3f, cycles per iteration %.0f, "
-          "empty-pool iterations %.3f" % (v["ww_walker_lanes"] / v["ww_walker_iters"],
-                                          v["ww_walker_admin_cycles"] / max(v["ww_walker_cycles"], 1),
-                                          v["ww_walker_cycles"] / v["ww_walker_iters"],
-                                          v["ww_walker_empty_iters"] / v["ww_walker_iters"]))
-    print("  tracer: pending lanes per iteration %.1f, ready lanes per iteration %.1f, iterations without a ready "
-          "lane %.3f, cycles per iteration %.0f" % (v["ww_tracer_pending"] / v["ww_tracer_iters"],
-                                                     v["ww_tracer_ready"] / v["ww_tracer_iters"],
-                                                     v["ww_tracer_idle_iters"] / v["ww_tracer_iters"],
-                                                     v["ww_tracer_cycles"] / v["ww_tracer_iters"]))
+it = max(v["wave_iterations"], 1)
+print("  lanes per wave iteration: shade %.1f, pending %.1f, starving %.1f, finished %.1f, prims %.1f" % (
+    v["lanes_ready"] / it, v["lanes_pending"] / it, v["lanes_starving"] / it, v["lanes_finished"] / it,
+    v["lanes_prims"] / it))
+print("  walk loop: node-section cycles %.3f, leaf-section cycles %.3f of walk-loop cycles; leaf sections per "
+      "wave loop iteration %.2f" % (v["cyc_walk_node"] / max(v["cyc_walk_loops"], 1),
+                                     v["cyc_walk_leaf"] / max(v["cyc_walk_loops"], 1),
+                                     v["walk_leaf_sections"] / max(v["walk_loop_wave_iters"], 1)))
