@@ -274,6 +274,7 @@ struct HostScene {
     int32_t run_end[5] = {};
     int flags = 0;
     uint32_t n_list = 0, n_grp = 0, n_tri = 0;
+    int32_t n_planes_y = 0;
 };
 
 int prepare_scene(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri, const void* groups,
@@ -362,6 +363,19 @@ int prepare_scene(const void* objects, uint32_t n_obj, const void* triangles, ui
             hs.spheres.push_back(r);
         }
     }
+    // The leading planes (list order kept) whose row 1 has +-0 x and z entries, and the
+    // parallel pairs (identical row1[0..2]) as the affine plane loops pair the planes:
+    // (0,1), (2,3), ... below n_planes_y, then on from there (find_closest_prims).
+    {
+        const int np = (int)hs.planes.size();
+        int npy = 0;
+        while (npy < np && hs.planes[npy].row1[0] == 0.0 && hs.planes[npy].row1[2] == 0.0) npy++;
+        hs.n_planes_y = npy;
+        auto same = [&](int a, int b) { return std::memcmp(hs.planes[a].row1, hs.planes[b].row1, 24) == 0; };
+        int p = 0;
+        for (; p + 1 < npy; p += 2) hs.planes[p].par = same(p, p + 1);
+        for (; p + 1 < np; p += 2) hs.planes[p].par = same(p, p + 1);
+    }
     hs.n_list = n_obj;
     hs.n_grp = n_grp;
     hs.n_tri = n_tri;
@@ -409,11 +423,7 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     for (int t = 0; t < 5; t++) s->dev.run_end[t] = hs.run_end[t];
     s->dev.planes = (const PlaneRec*)s->buffers[5];
     s->dev.n_planes = (int32_t)hs.planes.size();
-    // the leading planes (list order kept) whose row 1 has +-0 x and z entries
-    s->dev.n_planes_y = 0;
-    while (s->dev.n_planes_y < s->dev.n_planes && hs.planes[s->dev.n_planes_y].row1[0] == 0.0 &&
-           hs.planes[s->dev.n_planes_y].row1[2] == 0.0)
-        s->dev.n_planes_y++;
+    s->dev.n_planes_y = hs.n_planes_y;
     s->dev.spheres = (const SphereRec*)s->buffers[6];
     s->dev.n_spheres_st = (int32_t)hs.spheres.size();
     // HIP failures from here on release the half-built scene.

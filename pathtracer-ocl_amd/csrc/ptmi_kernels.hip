@@ -796,6 +796,16 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         q = (PTMI_ABLATE & 64) ? -oy * __builtin_amdgcn_rcp(dy) : A ? div_core(-oy, dy) : -oy / dy;  // DIAGNOSTIC 64
         ok = (fabs(dy) > kEps) & (q > kEps);
     };
+    // Two parallel planes (identical row1[0..2], affine: P.par): the same dy, so the
+    // divide core's reciprocal is shared (div_core_r; bit-identical to two div_cores).
+    auto plane_q2 = [&](double oy0, double oy1, double dy, double& q0, bool& k0, double& q1, bool& k1) {
+        const double r = rcp_core(dy);
+        q0 = div_core_r(-oy0, dy, r);
+        q1 = div_core_r(-oy1, dy, r);
+        const bool big = fabs(dy) > kEps;
+        k0 = big & (q0 > kEps);
+        k1 = big & (q1 > kEps);
+    };
     auto plane_t = [&](const PlaneRec& P, double& q, bool& ok) {
         double oy, dy;
         plane_rows(P, oy, dy);
@@ -817,10 +827,18 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
             const PlaneRec P0 = S.planes[p], P1 = S.planes[p + 1];
             double oy0, dy0, oy1, dy1, q0, q1;
             bool k0, k1;
-            plane_rows_nz<2>(P0.row1, ro, rd, oy0, dy0);
-            plane_rows_nz<2>(P1.row1, ro, rd, oy1, dy1);
-            plane_q(oy0, dy0, q0, k0);
-            plane_q(oy1, dy1, q1, k1);
+            if (P0.par) {  // parallel pair: one product m1 y, one direction term, one reciprocal
+                const double a = P0.row1[1] * ro.y;
+                oy0 = a + P0.row1[3];
+                oy1 = a + P1.row1[3];
+                dy0 = P0.row1[1] * rd.y;
+                plane_q2(oy0, oy1, dy0, q0, k0, q1, k1);
+            } else {
+                plane_rows_nz<2>(P0.row1, ro, rd, oy0, dy0);
+                plane_rows_nz<2>(P1.row1, ro, rd, oy1, dy1);
+                plane_q(oy0, dy0, q0, k0);
+                plane_q(oy1, dy1, q1, k1);
+            }
             plane_take(P0, q0, k0);
             plane_take(P1, q1, k1);
         }
@@ -829,10 +847,19 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         const PlaneRec P0 = S.planes[p], P1 = S.planes[p + 1];
         double oy0, dy0, oy1, dy1, q0, q1;
         bool k0, k1;
-        plane_rows(P0, oy0, dy0);
-        plane_rows(P1, oy1, dy1);
-        plane_q(oy0, dy0, q0, k0);
-        plane_q(oy1, dy1, q1, k1);
+        if (A && P0.par) {  // parallel pair: one sum of the origin's x, y, z terms, one direction term
+            const double* m = P0.row1;  // and one reciprocal (row1[0..2] of P1 are the same bits)
+            const double a = (m[0] * ro.x + m[1] * ro.y) + m[2] * ro.z;
+            oy0 = a + m[3];
+            oy1 = a + P1.row1[3];
+            dy0 = (m[0] * rd.x + m[1] * rd.y) + m[2] * rd.z;
+            plane_q2(oy0, oy1, dy0, q0, k0, q1, k1);
+        } else {
+            plane_rows(P0, oy0, dy0);
+            plane_rows(P1, oy1, dy1);
+            plane_q(oy0, dy0, q0, k0);
+            plane_q(oy1, dy1, q1, k1);
+        }
         plane_take(P0, q0, k0);
         plane_take(P1, q1, k1);
     }
