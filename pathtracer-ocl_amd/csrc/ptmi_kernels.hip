@@ -561,6 +561,27 @@ __device__ __forceinline__ bool cull_box(d4 o, d4 r, double mnx, double mny, dou
     return tn > tf || tn > lim || tf + prune_margin(tf) < kEps;
 }
 
+// walk_index's FP32 ray setup: with of = (float)o, rf = (float)(1/d) (|rf| clamped to
+// 1e30) and t' = fma(b, rf, -RN(of*rf)), the computed slab bound differs from the exact
+// (b - o)/d by at most 2^-23 |r| (|b| + 2|o|) (FP32 roundings of o, r, the product and
+// the fma); each axis interval is widened by dt = 4x that, so the test only rejects
+// boxes the exact line misses.
+__device__ __forceinline__ void walk_setup(d4 o, d4 rw, float bmax, float rf[3], float ofr[3], float dt[3]) {
+    const double oo[3] = {o.x, o.y, o.z}, rr[3] = {rw.x, rw.y, rw.z};
+    float omax = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float of = (float)oo[a];
+        const float r = (float)rr[a];  // rcp_walk: within 2^-40 of 1/d before the float rounding
+        rf[a] = fminf(fmaxf(r, -1e30f), 1e30f);  // NaN stays NaN
+        ofr[a] = of * rf[a];
+        omax = fmaxf(omax, fabsf(of));
+    }
+    const float E = 0x1p-21f * (bmax + 2.0f * omax) + 0x1p-120f;
+#pragma unroll
+    for (int a = 0; a < 3; a++) dt[a] = E * fabsf(rf[a]);
+}
+
 // Closest-hit walk of one root's 4-wide traversal index (ptmi_bvh.cpp): nearest
 // child first, the others pushed far-to-near.  Which triangles are FOUND does
 // not depend on the visiting order or the widened boxes (every triangle that
@@ -569,25 +590,8 @@ template <bool kVerify>
 __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes,
                                            const RootRec& R, int slot, int key, d4 o, d4 d, d4 rw, Hit& h,
                                            int& vchain) {
-    // FP32 slab tests.  With of = (float)o, rf = (float)(1/d) (|rf| clamped to
-    // 1e30) and t' = fma(b, rf, -RN(of*rf)), the computed slab bound differs from
-    // the exact (b - o)/d by at most 2^-23 |r| (|b| + 2|o|) (FP32 roundings of o,
-    // r, the product and the fma); each axis interval is widened by 4x that, so
-    // the test only rejects boxes the exact line misses.
-    float of[3], rf[3], ofr[3], dt[3];
-    const double oo[3] = {o.x, o.y, o.z}, rr[3] = {rw.x, rw.y, rw.z};
-    float omax = 0.0f;
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-        of[a] = (float)oo[a];
-        const float r = (float)rr[a];  // rcp_walk: within 2^-40 of 1/d before the float rounding
-        rf[a] = fminf(fmaxf(r, -1e30f), 1e30f);  // NaN stays NaN
-        ofr[a] = of[a] * rf[a];
-        omax = fmaxf(omax, fabsf(of[a]));
-    }
-    const float E = 0x1p-21f * (R.bmax + 2.0f * omax) + 0x1p-120f;
-#pragma unroll
-    for (int a = 0; a < 3; a++) dt[a] = E * fabsf(rf[a]);
+    float rf[3], ofr[3], dt[3];  // FP32 slab tests (walk_setup)
+    walk_setup(o, rw, R.bmax, rf, ofr, dt);
     int sp = 0;
     int cur = R.entry;
     PTMI_COUNT(0);
