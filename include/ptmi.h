@@ -155,8 +155,11 @@ int ptmi_scene_size(const ptmi_scene* s, uint32_t* width, uint32_t* height);
  *                (A = number of samples) for owned pixels, 0 for the others.
  *   tile_stride/tile_offset: pixel ownership for a tile split -- 8x8 tile t is
  *                owned when t % tile_stride == tile_offset (1/0 = all pixels).
- *   chunks     : sample chunks per pixel (load balance; 0 = auto).  Chunk sums
- *                are combined in a fixed order, so results are deterministic.
+ *   chunks     : sample chunks per pixel for every owned tile (load balance), or
+ *                0 = auto: most tiles are one work item over the whole range
+ *                (summed in sample order), the tiles at the end of the launch are
+ *                split into chunks.  Chunk sums are combined in a fixed order, so
+ *                results are deterministic.
  * Sample indices are GLOBAL (fgi2 = seed/samples and the DoF aperture pattern
  * depend on n and on the total, tracer.cl:841, 766), so any split of
  * [0, samples) sums to the same frame.

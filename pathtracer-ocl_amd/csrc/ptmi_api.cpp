@@ -21,12 +21,10 @@
 #include "ptmi_device.h"
 
 namespace ptmi {
-hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, uint32_t s_begin, uint32_t s_end,
-                        uint32_t chunk_len, uint32_t nchunks, uint32_t tile_stride, uint32_t tile_offset,
-                        const double* seeds, const double* sunf, double* out, hipStream_t st);
+hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const double* seeds,
+                        const double* sunf, double* sums, double* part, hipStream_t st);
 hipError_t launch_sunflower(double* out, uint32_t samples, hipStream_t st);
-hipError_t launch_reduce(const double* part, double* sums, uint32_t npix, uint32_t nchunks, int W, int H,
-                         uint32_t tile_stride, uint32_t tile_offset, hipStream_t st);
+hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, int W, int H, hipStream_t st);
 hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint32_t samples, hipStream_t st);
 hipError_t launch_seeds(double* seeds, uint32_t n, uint64_t stream, hipStream_t st);
 hipError_t launch_plane_normals(DevObject* objs, int n, hipStream_t st);
@@ -48,6 +46,7 @@ struct ptmi_scene {
     uint32_t sunf_samples = 0;
     size_t partial_bytes = 0;
     int resident_waves = 0;  // device-wide resident waves of trace_kernel
+    uint32_t tail_tiles = 0;  // chunked tiles at the end of an automatic launch; 0: default (see render)
     uint32_t width = 0, height = 0;
     int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
     bool timing = false;
@@ -452,7 +451,7 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     s->dev.n_list = hs.n_list;
     s->dev.n_nodes = hs.n_grp;
     s->dev.n_nodes4 = (int32_t)hs.index.nodes.size();
-    s->dev.steal = getenv("PTMI_NO_STEAL") ? 0u : 1u;  // testing: per-lane sample order as without stealing
+    if (const char* t = getenv("PTMI_TAIL_TILES")) s->tail_tiles = (uint32_t)atoi(t);  // testing: small frames with whole tiles
     s->dev.n_tri = hs.n_tri;
     s->dev.cam = hs.cam;
     hipDeviceProp_t p;
@@ -551,19 +550,39 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     const uint32_t range = sample_end - sample_begin;
     const uint32_t tiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
     const uint32_t owned_tiles = (tiles + tile_stride - 1 - tile_offset) / tile_stride;
+    // Work items (WorkPlan, ptmi_device.h).  Automatic (chunks == 0), scenes without
+    // meshes: whole tiles first, then the last ~0.5 resident waves' worth of tiles
+    // split into sample chunks, so that short items fill the end of the launch (~8 per
+    // resident wave slot, >= 32 samples each).  A whole-tile item pays its start-up
+    // and the spread of its lanes' path lengths once for the whole range, and sums in
+    // sample order without a partial buffer.  C2 (2048 spp, 4096 resident waves): 185.3 ms
+    // with every tile chunked; 181.6 / 178.2 / 177.5 / 176.8 / 182.5 ms with 9000 / 4096 /
+    // 3072 / 2048 / 1024 chunked tail tiles.
+    // Mesh scenes chunk every tile (~32 items per slot): a tile's cost there depends on
+    // how much mesh it sees, so whole tiles leave a long tail (C4 801 -> 1008 ms).
+    // An explicit chunk count splits every tile.
+    WorkPlan wp{};
+    wp.s_begin = sample_begin;
+    wp.s_end = sample_end;
+    wp.tile_stride = tile_stride;
+    wp.tile_offset = tile_offset;
+    uint32_t n_tail = owned_tiles;
     if (chunks == 0) {
-        // ~32 work items (tile x sample chunk) per resident wave slot, >= 32 samples per
-        // chunk: short items shorten the end-of-launch tail, while each item pays a fixed
-        // start-up.  Measured (one MI355X, 2048 spp): C2 242.7 ms at 2 chunks, 234.5 at 7,
-        // 233.3 at 12; teapot 922 / 862 / 885 ms at 2 / 6 / 16; gopher 1484 / 1404 / 1416.
-        // The 256-sample range of one rank of 8: 23.85 / 23.46 / 23.38 ms at 2 / 4 / 8 chunks.
-        const uint64_t want = (uint64_t)s->resident_waves * 32;
-        chunks = (uint32_t)std::min<uint64_t>((want + owned_tiles - 1) / std::max<uint32_t>(owned_tiles, 1),
+        const bool mesh = (s->flags & 1) != 0;  // F_GROUPS
+        if (!mesh || s->tail_tiles)
+            n_tail = std::min<uint32_t>(owned_tiles, s->tail_tiles ? s->tail_tiles : (uint32_t)(s->resident_waves / 2));
+        const uint64_t want = (uint64_t)s->resident_waves * (mesh ? 32 : 8);
+        chunks = (uint32_t)std::min<uint64_t>((want + n_tail - 1) / std::max<uint32_t>(n_tail, 1),
                                               std::max<uint32_t>(range / 32, 1));
     }
     chunks = std::max<uint32_t>(1, std::min<uint32_t>(chunks, std::max<uint32_t>(range, 1)));
     const uint32_t chunk_len = range == 0 ? 1 : (range + chunks - 1) / chunks;
     chunks = range == 0 ? 1 : (range + chunk_len - 1) / chunk_len;
+    if (chunks == 1) n_tail = 0;  // one chunk: every tile is whole
+    wp.n_whole = owned_tiles - n_tail;
+    wp.n_tail = n_tail;
+    wp.nchunks = chunks;
+    wp.chunk_len = chunk_len;
     if ((s->flags & 8) && s->dev.cam.aperture != 0 && s->sunf_samples != samples) {  // DoF table for this S
         if (s->sunf) {
             HIP_TRY(hipStreamSynchronize(st));
@@ -585,18 +604,8 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
             }
         }
     }
-    if (chunks == 1) {
-        if (tile_stride > 1) HIP_TRY(hipMemsetAsync(sums_dev, 0, (size_t)npix * 4 * sizeof(double), st));
-        if (ev0) HIP_TRY(hipEventRecord(ev0, st));
-        HIP_TRY(launch_trace(s->dev, s->flags, samples, sample_begin, sample_end, chunk_len, 1, tile_stride, tile_offset,
-                             seeds_dev, s->sunf, sums_dev, st));
-        if (ev1) {
-            HIP_TRY(hipEventRecord(ev1, st));
-            s->events.emplace_back(ev0, ev1);
-        }
-        return PTMI_OK;
-    }
-    const size_t need = (size_t)chunks * npix * 4 * sizeof(double);
+    if (tile_stride > 1) HIP_TRY(hipMemsetAsync(sums_dev, 0, (size_t)npix * 4 * sizeof(double), st));  // un-owned tiles
+    const size_t need = (size_t)wp.n_tail * 64 * chunks * 4 * sizeof(double);
     if (need > s->partial_bytes) {
         if (s->partial) {
             HIP_TRY(hipStreamSynchronize(st));
@@ -608,13 +617,12 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         s->partial_bytes = need;
     }
     if (ev0) HIP_TRY(hipEventRecord(ev0, st));
-    HIP_TRY(launch_trace(s->dev, s->flags, samples, sample_begin, sample_end, chunk_len, chunks, tile_stride, tile_offset,
-                         seeds_dev, s->sunf, s->partial, st));
+    HIP_TRY(launch_trace(s->dev, s->flags, samples, wp, seeds_dev, s->sunf, sums_dev, s->partial, st));
     if (ev1) {
         HIP_TRY(hipEventRecord(ev1, st));
         s->events.emplace_back(ev0, ev1);
     }
-    HIP_TRY(launch_reduce(s->partial, sums_dev, npix, chunks, (int)W, (int)H, tile_stride, tile_offset, st));
+    HIP_TRY(launch_reduce(s->partial, sums_dev, wp, (int)W, (int)H, st));
     return PTMI_OK;
 }
 

@@ -149,11 +149,25 @@ struct DevScene {
     uint32_t n_obj;   // intersectable objects in objs[]
     uint32_t n_nodes, n_tri;
     uint32_t n_list;  // numObjects of the reference's list (fgi = seed / numObjects, tracer.cl:840)
-    uint32_t steal;   // segment stealing in BVH scenes (trace_kernel); 0: off (PTMI_NO_STEAL, A/B and tests)
     DevCamera cam;
     DevTexArray tex[3];  // textures, sphereTextures, cubeMapTextures (tracer.cl:833)
 };
 
 constexpr int kTile = 8;          // a wave64 covers an 8x8 pixel tile
+
+// One launch's work items (trace_kernel, by value).  The owned tiles are
+// tile_offset + k * tile_stride, k = 0, 1, ...  The first n_whole of them are one
+// item each over the whole sample range [s_begin, s_end), summed straight into the
+// frame; the last n_tail are split into nchunks sample chunks of chunk_len, one
+// item each, whose sums go to a partial buffer (chunk-major: chunk c of tail tile
+// tt at [(c * n_tail + tt) * 64 + lane]) that reduce_chunks_kernel adds up in
+// chunk order.  Items are numbered whole tiles first, so the short chunk items
+// fill the end of the launch.
+struct WorkPlan {
+    uint32_t s_begin, s_end;
+    uint32_t tile_stride, tile_offset;
+    uint32_t n_whole, n_tail;
+    uint32_t nchunks, chunk_len;
+};
 
 }  // namespace ptmi

@@ -100,13 +100,6 @@ static constexpr int kRefillNeed = PTMI_REFILL_NEED;
 #define PTMI_WALK_BATCH 24
 #endif
 static constexpr int kWalkBatch = PTMI_WALK_BATCH;  // parked lanes that trigger a wave's BVH walk phase
-#ifndef PTMI_STEAL
-#define PTMI_STEAL 1  // finished lanes take over samples of busy lanes of the wave (trace_kernel)
-#endif
-#ifndef PTMI_STEAL_MIN
-#define PTMI_STEAL_MIN 2  // a lane is stolen from when it has at least this many samples not started
-#endif
-static constexpr uint32_t kStealMin = PTMI_STEAL_MIN;
 #ifndef PTMI_SPHERE_RCP
 #define PTMI_SPHERE_RCP 1  // both sphere roots from one reciprocal (sphere_roots)
 #endif
@@ -586,56 +579,42 @@ __device__ __forceinline__ void walk_setup(d4 o, d4 rw, float bmax, float rf[3],
 // child first, the others pushed far-to-near.  Which triangles are FOUND does
 // not depend on the visiting order or the widened boxes (every triangle that
 // can produce a winning t is reached); ties resolve through better_tri.
-template <bool kVerify>
-__device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes,
-                                           const RootRec& R, int slot, int key, d4 o, d4 d, d4 rw, Hit& h,
-                                           int& vchain) {
-    float rf[3], ofr[3], dt[3];  // FP32 slab tests (walk_setup)
-    walk_setup(o, rw, R.bmax, rf, ofr, dt);
-    int sp = 0;
-    int cur = R.entry;
-    PTMI_COUNT(0);
-#if PTMI_STATS == 1
-    int st_nodes = 0, st_leaves = 0;
-    const double st_t0 = h.t;
-#endif
-    while (true) {
-        PTMI_COUNT_ACTIVE(19);  // (stats: wave-level walk loop iterations)
-        PTMI_TSTAMP(t_nd);
-        if (cur >= 0) {
-            PTMI_COUNT(1);
-#if PTMI_STATS == 1
-            st_nodes++;
-#endif
-            // The node's 112 B as seven 16-B loads issued together (one wait), from LDS
-            // for the first kLdsNodes Node4s (the top levels, ptmi_bvh.cpp), else global.
-            const float4* src = cur < kLdsNodes ? reinterpret_cast<const float4*>(lds_nodes) + 7 * cur
-                                                : reinterpret_cast<const float4*>(S.nodes4) + 7 * cur;
-            float4 q[7];
+// One Node4 of a walk: its four children tested against the FP32 slabs, the hit
+// ones ordered near-to-far; the far ones are pushed (farthest first) and the
+// nearest is returned in `next` (false: no child hit, pop the stack).
+__device__ __forceinline__ bool node_visit(const DevScene& S, const Node4* lds_nodes, int* __restrict__ stk, int cur,
+                                           int& sp, const float rf[3], const float ofr[3], const float dt[3],
+                                           double ht, int& next) {
+    PTMI_COUNT(1);
+    // The node's 112 B as seven 16-B loads issued together (one wait), from LDS
+    // for the first kLdsNodes Node4s (the top levels, ptmi_bvh.cpp), else global.
+    const float4* src = cur < kLdsNodes ? reinterpret_cast<const float4*>(lds_nodes) + 7 * cur
+                                        : reinterpret_cast<const float4*>(S.nodes4) + 7 * cur;
+    float4 q[7];
 #pragma unroll
-            for (int u = 0; u < 7; u++) q[u] = src[u];
-            const float mnx[4] = {q[0].x, q[0].y, q[0].z, q[0].w}, mny[4] = {q[1].x, q[1].y, q[1].z, q[1].w};
-            const float mnz[4] = {q[2].x, q[2].y, q[2].z, q[2].w}, mxx[4] = {q[3].x, q[3].y, q[3].z, q[3].w};
-            const float mxy[4] = {q[4].x, q[4].y, q[4].z, q[4].w}, mxz[4] = {q[5].x, q[5].y, q[5].z, q[5].w};
-            const int ch[4] = {__float_as_int(q[6].x), __float_as_int(q[6].y), __float_as_int(q[6].z),
-                               __float_as_int(q[6].w)};
-            const double limd = h.t + prune_margin(h.t);
-            const float lim = (float)limd * (1.0f + 0x1p-22f) + 0x1p-100f;  // >= limd
-            float k[4];
-            int c[4];
+    for (int u = 0; u < 7; u++) q[u] = src[u];
+    const float mnx[4] = {q[0].x, q[0].y, q[0].z, q[0].w}, mny[4] = {q[1].x, q[1].y, q[1].z, q[1].w};
+    const float mnz[4] = {q[2].x, q[2].y, q[2].z, q[2].w}, mxx[4] = {q[3].x, q[3].y, q[3].z, q[3].w};
+    const float mxy[4] = {q[4].x, q[4].y, q[4].z, q[4].w}, mxz[4] = {q[5].x, q[5].y, q[5].z, q[5].w};
+    const int ch[4] = {__float_as_int(q[6].x), __float_as_int(q[6].y), __float_as_int(q[6].z),
+                       __float_as_int(q[6].w)};
+    const double limd = ht + prune_margin(ht);
+    const float lim = (float)limd * (1.0f + 0x1p-22f) + 0x1p-100f;  // >= limd
+    float k[4];
+    int c[4];
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                c[i] = ch[i];
-                const float ax = fmaf(mnx[i], rf[0], -ofr[0]), bx = fmaf(mxx[i], rf[0], -ofr[0]);
-                const float ay = fmaf(mny[i], rf[1], -ofr[1]), by = fmaf(mxy[i], rf[1], -ofr[1]);
-                const float az = fmaf(mnz[i], rf[2], -ofr[2]), bz = fmaf(mxz[i], rf[2], -ofr[2]);
-                const float tn = fmaxf(fmaxf(fminf(ax, bx) - dt[0], fminf(ay, by) - dt[1]), fminf(az, bz) - dt[2]);
-                const float tf = fminf(fminf(fmaxf(ax, bx) + dt[0], fmaxf(ay, by) + dt[1]), fmaxf(az, bz) + dt[2]);
-                // (NaN bounds -- a NaN ray -- fail every test: the child is entered.)
-                const bool cull = tn > tf || tn > lim || tf < 0.0f || c[i] == kEmptyChild;
-                k[i] = cull ? __builtin_huge_valf() : fmaxf(tn, -__builtin_huge_valf());  // NaN -> -inf
-            }
-            // sort (k, c) ascending: 5 compare-exchanges
+    for (int i = 0; i < 4; i++) {
+        c[i] = ch[i];
+        const float ax = fmaf(mnx[i], rf[0], -ofr[0]), bx = fmaf(mxx[i], rf[0], -ofr[0]);
+        const float ay = fmaf(mny[i], rf[1], -ofr[1]), by = fmaf(mxy[i], rf[1], -ofr[1]);
+        const float az = fmaf(mnz[i], rf[2], -ofr[2]), bz = fmaf(mxz[i], rf[2], -ofr[2]);
+        const float tn = fmaxf(fmaxf(fminf(ax, bx) - dt[0], fminf(ay, by) - dt[1]), fminf(az, bz) - dt[2]);
+        const float tf = fminf(fminf(fmaxf(ax, bx) + dt[0], fmaxf(ay, by) + dt[1]), fmaxf(az, bz) + dt[2]);
+        // (NaN bounds -- a NaN ray -- fail every test: the child is entered.)
+        const bool cull = tn > tf || tn > lim || tf < 0.0f || c[i] == kEmptyChild;
+        k[i] = cull ? __builtin_huge_valf() : fmaxf(tn, -__builtin_huge_valf());  // NaN -> -inf
+    }
+    // sort (k, c) ascending: 5 compare-exchanges
 #define PTMI_CX(a, b)                                      \
     if (k[b] < k[a]) {                                     \
         const float tk = k[a];                             \
@@ -645,41 +624,62 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
         c[a] = c[b];                                       \
         c[b] = tc;                                         \
     }
-            PTMI_CX(0, 1) PTMI_CX(2, 3) PTMI_CX(0, 2) PTMI_CX(1, 3) PTMI_CX(1, 2)
+    PTMI_CX(0, 1) PTMI_CX(2, 3) PTMI_CX(0, 2) PTMI_CX(1, 3) PTMI_CX(1, 2)
 #undef PTMI_CX
-            if (k[3] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[3];
-            if (k[2] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[2];
-            if (k[1] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[1];
+    if (k[3] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[3];
+    if (k[2] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[2];
+    if (k[1] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[1];
+    next = c[0];
+    return k[0] < __builtin_huge_valf();
+}
+
+// The triangles of one leaf (code = first << 3 | count).
+template <bool kVerify>
+__device__ __forceinline__ void leaf_visit(const DevScene& S, int code, int slot, int key, d4 o, d4 d, Hit& h,
+                                           int& vchain) {
+    PTMI_WADD(31, 1ull);
+    const int first = code >> 3, end = first + (code & 7);
+    PTMI_COUNT(2);
+    for (int i = first; i < end; i++) {
+        PTMI_COUNT(3);
+#if !(defined(PTMI_EXP) && (PTMI_EXP & 4))
+        tri_test<kVerify>(S, S.tris[i], o, d, slot, key, h, vchain);
+#endif
+    }
+}
+
+// Closest-hit walk of one root's 4-wide traversal index (ptmi_bvh.cpp): nearest
+// child first, the others pushed far-to-near.  Which triangles are FOUND does
+// not depend on the visiting order or the widened boxes (every triangle that
+// can produce a winning t is reached); ties resolve through better_tri.
+template <bool kVerify>
+__device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes,
+                                           const RootRec& R, int slot, int key, d4 o, d4 d, d4 rw, Hit& h,
+                                           int& vchain) {
+    float rf[3], ofr[3], dt[3];  // FP32 slab tests (walk_setup)
+    walk_setup(o, rw, R.bmax, rf, ofr, dt);
+    int sp = 0;
+    int cur = R.entry;
+    PTMI_COUNT(0);
+    while (true) {
+        PTMI_COUNT_ACTIVE(19);  // (stats: wave-level walk loop iterations)
+        PTMI_TSTAMP(t_nd);
+        if (cur >= 0) {
+            int next;
+            const bool down = node_visit(S, lds_nodes, stk, cur, sp, rf, ofr, dt, h.t, next);
             PTMI_TADD(29, t_nd);
-            if (k[0] < __builtin_huge_valf()) {
-                cur = c[0];
+            if (down) {
+                cur = next;
                 continue;
             }
         } else if (cur != kEmptyChild) {
             PTMI_TSTAMP(t_lf);
-            PTMI_WADD(31, 1ull);
-            const int code = -cur - 1;
-            const int first = code >> 3, end = first + (code & 7);
-            PTMI_COUNT(2);
-#if PTMI_STATS == 1
-            st_leaves++;
-#endif
-            for (int i = first; i < end; i++) {
-                PTMI_COUNT(3);
-#if !(defined(PTMI_EXP) && (PTMI_EXP & 4))
-                tri_test<kVerify>(S, S.tris[i], o, d, slot, key, h, vchain);
-#endif
-            }
+            leaf_visit<kVerify>(S, -cur - 1, slot, key, o, d, h, vchain);
             PTMI_TADD(30, t_lf);
         }
         if (sp == 0) break;
         cur = stk[(--sp) * kStkStride];
     }
-#if PTMI_STATS == 1
-    if (st_leaves == 0) PTMI_COUNT(20);  // (stats: walks that reach no leaf)
-    if (st_leaves == 0 && st_nodes <= 1) PTMI_COUNT(21);  // (... that end at the root node)
-    if (h.t < st_t0) PTMI_COUNT(22);  // (... that improve the best hit)
-#endif
 }
 
 // Candidate update as selects (no exec-mask branching).  t > EPSILON implies
@@ -1064,28 +1064,6 @@ __device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__
         }
     }
 #endif
-}
-
-// Position of the r-th (0-based) set bit of m (r < popc(m)).
-__device__ __forceinline__ int nth_set_bit(unsigned long long m, int r) {
-    uint32_t w = (uint32_t)m;
-    int base = 0;
-    int pc = __popc(w);
-    if (r >= pc) {
-        r -= pc;
-        w = (uint32_t)(m >> 32);
-        base = 32;
-    }
-#pragma unroll
-    for (int span = 16; span >= 1; span >>= 1) {
-        pc = __popc(w & ((1u << span) - 1u));
-        if (r >= pc) {
-            r -= pc;
-            w >>= span;
-            base += span;
-        }
-    }
-    return base;
 }
 
 // schlick (tracer.cl:485-505)
@@ -1500,10 +1478,9 @@ template <int FL>
 #ifndef PTMI_WAVES_GROUPS
 #define PTMI_WAVES_GROUPS 3  // ... and with BVH groups (the walk needs more registers; 4 spills)
 #endif
-__global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, uint32_t s_begin, uint32_t s_end,
-                                                    uint32_t chunk_len, uint32_t tile_stride, uint32_t tile_offset,
+__global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, WorkPlan WP,
                                                     const double* __restrict__ seeds, const double* __restrict__ sunf,
-                                                    double* __restrict__ out) {
+                                                    double* __restrict__ sums, double* __restrict__ part) {
     // Top levels of the traversal index in LDS (group scenes), staged by the whole
     // workgroup before any wave can leave.  Entries past n_nodes4 are never read.
     __shared__ float4 node_lds4[(FL & F_GROUPS) ? (kLdsNodes > 0 ? kLdsNodes : 1) * 7 : 1];
@@ -1521,54 +1498,41 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
     const int tiles_x = (W + kTile - 1) / kTile;
     const int tiles_y = (H + kTile - 1) / kTile;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tile = blockIdx.x * (kBlock / 64) + wave;
-    if (tile >= tiles_x * tiles_y) return;
-    if ((uint32_t)tile % tile_stride != tile_offset) return;
-    const int px0 = (tile % tiles_x) * kTile + (lane & 7);
-    const int py0 = (tile / tiles_x) * kTile + (lane >> 3);
+    // Work item -> (owned tile k, sample range, output slot): WorkPlan.
+    const uint32_t item = blockIdx.x * (kBlock / 64) + wave;
+    uint32_t k, c0, c1;
+    size_t oslot;  // output: pixel index into sums, or slot of the partial buffer
+    bool whole;
+    if (item < WP.n_whole) {
+        whole = true;
+        k = item;
+        c0 = WP.s_begin;
+        c1 = WP.s_end;
+    } else {
+        whole = false;
+        const uint32_t t = item - WP.n_whole;
+        const uint32_t c = t / max(WP.n_tail, 1u), tt = t - c * WP.n_tail;
+        if (c >= WP.nchunks) return;
+        k = WP.n_whole + tt;
+        c0 = WP.s_begin + c * WP.chunk_len;
+        c1 = min(WP.s_end, c0 + WP.chunk_len);
+        oslot = ((size_t)c * WP.n_tail + tt) * 64 + lane;
+    }
+    const uint32_t tile = WP.tile_offset + k * WP.tile_stride;
+    if (tile >= (uint32_t)(tiles_x * tiles_y)) return;
+    const int px0 = (int)(tile % (uint32_t)tiles_x) * kTile + (lane & 7);
+    const int py0 = (int)(tile / (uint32_t)tiles_x) * kTile + (lane >> 3);
     if (px0 >= W || py0 >= H) return;
     constexpr bool A = !(FL & F_PROJ);
     const uint32_t i = (uint32_t)py0 * (uint32_t)W + (uint32_t)px0;
-    const uint32_t c0 = s_begin + blockIdx.y * chunk_len;
-    const uint32_t c1 = min(s_end, c0 + chunk_len);
+    if (whole) oslot = i;
     // fgi / fgi2 (tracer.cl:839-841): double division rounded to float.
     const double seed = seeds[i];
-    // The lane's current segment: samples [n_gen .., c_end) of the pixel (px, py) whose
-    // sums are accumulated at acc_lds[owner].  It starts as the lane's own pixel and chunk;
-    // a lane that has finished takes the later half of the samples a busier lane has
-    // not started (see "Segment stealing" below).
-    int px = px0, py = py0, owner = lane;
-    float fgi = (float)(seed / (double)S.n_list);
-    float fgi2 = (float)(seed / (double)samples);
-    uint32_t c_end = c1;
-    double cr = 0.0, cg = 0.0, cb = 0.0;  // the current segment's sums
-    bool seg_open = true;                 // cr/cg/cb not yet added to acc_lds[owner]
-    // Per-pixel chunk sums of the wave's 64 pixels (lane-indexed, SoA) when stealing.
-    constexpr bool kSteal = PTMI_STEAL && (FL & F_GROUPS);
-    __shared__ double acc_lds[kSteal ? 3 * kBlock : 1];
-    double* acc = acc_lds + (threadIdx.x & ~63);
-    if constexpr (kSteal) {
-        acc[lane] = 0.0;
-        acc[64 + lane] = 0.0;
-        acc[128 + lane] = 0.0;
-    }
-    // Adds every finishing lane's segment sums into its owner's pixel sums, one lane at
-    // a time in lane order (two lanes may finish segments of the same pixel together):
-    // a fixed order, so the image is deterministic.
-    auto flush = [&](bool fin) {
-        unsigned long long m = __ballot(fin && seg_open);
-        while (m) {
-            const int k = __ffsll((long long)m) - 1;
-            if (lane == k) {
-                acc[owner] = acc[owner] + cr;
-                acc[64 + owner] = acc[64 + owner] + cg;
-                acc[128 + owner] = acc[128 + owner] + cb;
-                cr = cg = cb = 0.0;
-                seg_open = false;
-            }
-            m &= m - 1;
-        }
-    };
+    const int px = px0, py = py0;
+    const float fgi = (float)(seed / (double)S.n_list);
+    const float fgi2 = (float)(seed / (double)samples);
+    const uint32_t c_end = c1;
+    double cr = 0.0, cg = 0.0, cb = 0.0;  // colors (tracer.cl:1179)
     // Camera rays are produced in wave-wide batches into a kCamDepth-deep per-lane
     // ring buffer (LDS) and consumed by path regeneration: generating them at the
     // moment each lane needs one would run the camera block (2 noise3D + the
@@ -1597,41 +1561,6 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
     for (;;) {
         if (!__any(active || nb > 0 || n_gen < c_end)) break;
         PTMI_TSTAMP(t_a);
-        if constexpr (kSteal) {
-        // Segment stealing.  Lanes whose pixels need long paths (a mesh in view) keep
-        // a wave busy while the others have finished their chunk; each finished lane
-        // takes the later half of the samples a busy lane has not started.  The sum of
-        // a pixel's samples is then a sum of segment sums (like the chunk sums), in an
-        // order fixed by the wave's own execution.
-        if (S.steal) {
-            const bool fin = !active && nb == 0 && n_gen >= c_end;
-            const unsigned long long F = __ballot(fin);
-            if (F) {
-                flush(fin);
-                const uint32_t rem = n_gen < c_end ? c_end - n_gen : 0u;  // samples not yet started
-                const unsigned long long V = __ballot(rem >= kStealMin);
-                const int nt = min(__popcll(F), __popcll(V));
-                if (nt > 0) {
-                    const unsigned long long below = (1ull << lane) - 1ull;
-                    const int rf = __popcll(F & below), rv = __popcll(V & below);
-                    const bool thief = fin && rf < nt;
-                    const bool victim = !fin && rem >= kStealMin && rv < nt;
-                    const int src = thief ? nth_set_bit(V, rf) : lane;
-                    const int vx = __shfl(px, src), vy = __shfl(py, src), vo = __shfl(owner, src);
-                    const float vf = __shfl(fgi, src), vf2 = __shfl(fgi2, src);
-                    const uint32_t vg = (uint32_t)__shfl((int)n_gen, src), ve = (uint32_t)__shfl((int)c_end, src);
-                    const uint32_t mid = vg + ((ve - vg) - (ve - vg) / 2u);  // the victim keeps the larger half
-                    if (thief) {
-                        px = vx, py = vy, owner = vo, fgi = vf, fgi2 = vf2;
-                        n_gen = mid;
-                        c_end = ve;
-                        seg_open = true;
-                    }
-                    if (victim) c_end = mid;
-                }
-            }
-        }
-        }
         const bool need = nb < kCamDepth && n_gen < c_end;
         const int n_need = __popcll(__ballot(need));
         const int n_starve = __popcll(__ballot(nb == 0 && !active && n_gen < c_end));
@@ -1734,17 +1663,10 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
         for (int k = 0; k < 32; k++)
             if (ptmi_wstat[threadIdx.x >> 6][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[threadIdx.x >> 6][k]);
 #endif
-    double* o = out + ((size_t)blockIdx.y * ((size_t)W * H) + i) * 4;
-    if constexpr (kSteal) {
-        flush(true);
-        o[0] = acc[lane];
-        o[1] = acc[64 + lane];
-        o[2] = acc[128 + lane];
-    } else {
-        o[0] = cr;
-        o[1] = cg;
-        o[2] = cb;
-    }
+    double* o = (whole ? sums : part) + oslot * 4;
+    o[0] = cr;
+    o[1] = cg;
+    o[2] = cb;
     o[3] = (double)(c1 > c0 ? c1 - c0 : 0);
 }
 
@@ -1783,26 +1705,27 @@ hipError_t launch_plane_normals(DevObject* objs, int n, hipStream_t st) {
     return hipGetLastError();
 }
 
-// Sum chunk partials in chunk order (deterministic); zero un-owned pixels.
+// The tail tiles' chunk partials (WorkPlan) summed in chunk order (deterministic)
+// into the frame; one thread per tail-tile pixel.
 __global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __restrict__ part, double* __restrict__ sums,
-                                                            uint32_t npix, uint32_t nchunks, int W, int H,
-                                                            uint32_t tile_stride, uint32_t tile_offset) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= npix) return;
-    const int px = (int)(i % (uint32_t)W), py = (int)(i / (uint32_t)W);
+                                                            WorkPlan WP, int W, int H) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= WP.n_tail * 64) return;
+    const uint32_t tt = j >> 6, lane = j & 63;
     const int tiles_x = (W + kTile - 1) / kTile;
-    const uint32_t tile = (uint32_t)((py / kTile) * tiles_x + px / kTile);
+    const uint32_t tile = WP.tile_offset + (WP.n_whole + tt) * WP.tile_stride;
+    const int px = (int)(tile % (uint32_t)tiles_x) * kTile + (int)(lane & 7);
+    const int py = (int)(tile / (uint32_t)tiles_x) * kTile + (int)(lane >> 3);
+    if (px >= W || py >= H) return;
     double r = 0.0, g = 0.0, b = 0.0, a = 0.0;
-    if (tile % tile_stride == tile_offset) {
-        for (uint32_t c = 0; c < nchunks; c++) {
-            const double* p = part + ((size_t)c * npix + i) * 4;
-            r = r + p[0];
-            g = g + p[1];
-            b = b + p[2];
-            a = a + p[3];
-        }
+    for (uint32_t c = 0; c < WP.nchunks; c++) {
+        const double* p = part + ((size_t)c * WP.n_tail * 64 + j) * 4;
+        r = r + p[0];
+        g = g + p[1];
+        b = b + p[2];
+        a = a + p[3];
     }
-    double* o = sums + (size_t)i * 4;
+    double* o = sums + ((size_t)py * W + px) * 4;
     o[0] = r;
     o[1] = g;
     o[2] = b;
@@ -1870,27 +1793,26 @@ const void* trace_kernel_symbol(int flags) {
     return nullptr;
 }
 
-hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, uint32_t s_begin, uint32_t s_end,
-                        uint32_t chunk_len, uint32_t nchunks, uint32_t tile_stride, uint32_t tile_offset,
-                        const double* seeds, const double* sunf, double* out, hipStream_t st) {
-    const int tiles = ((S.cam.width + kTile - 1) / kTile) * ((S.cam.height + kTile - 1) / kTile);
+hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const double* seeds,
+                        const double* sunf, double* sums, double* part, hipStream_t st) {
     constexpr int wpb = kBlock / 64;
-    const dim3 grid((tiles + wpb - 1) / wpb, nchunks);
+    const uint32_t items = WP.n_whole + WP.n_tail * WP.nchunks;
+    if (items == 0) return hipSuccess;
+    const dim3 grid((items + wpb - 1) / wpb);
     if (flags & F_TEX) {  // textured scene: the generic instantiation plus the texture lookups
-        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ | F_TEX>, grid, dim3(kBlock), 0, st, S, samples, s_begin, s_end,
-                           chunk_len, tile_stride, tile_offset, seeds, sunf, out);
+        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ | F_TEX>, grid, dim3(kBlock), 0, st, S, samples, WP, seeds, sunf,
+                           sums, part);
         return hipGetLastError();
     }
     if (flags & F_PROJ) {  // non-affine scene: one generic instantiation with the literal w arithmetic
-        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ>, grid, dim3(kBlock), 0, st, S, samples, s_begin, s_end,
-                           chunk_len, tile_stride, tile_offset, seeds, sunf, out);
+        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ>, grid, dim3(kBlock), 0, st, S, samples, WP, seeds, sunf, sums,
+                           part);
         return hipGetLastError();
     }
     switch (flags & F_ALL) {
-#define K(f)                                                                                                   \
-    case f:                                                                                                    \
-        hipLaunchKernelGGL(trace_kernel<f>, grid, dim3(kBlock), 0, st, S, samples, s_begin, s_end, chunk_len,  \
-                           tile_stride, tile_offset, seeds, sunf, out);                                        \
+#define K(f)                                                                                                  \
+    case f:                                                                                                   \
+        hipLaunchKernelGGL(trace_kernel<f>, grid, dim3(kBlock), 0, st, S, samples, WP, seeds, sunf, sums, part); \
         break;
         K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15)
 #undef K
@@ -1898,10 +1820,10 @@ hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, uint32_t
     return hipGetLastError();
 }
 
-hipError_t launch_reduce(const double* part, double* sums, uint32_t npix, uint32_t nchunks, int W, int H,
-                         uint32_t tile_stride, uint32_t tile_offset, hipStream_t st) {
-    hipLaunchKernelGGL(reduce_chunks_kernel, dim3((npix + 255) / 256), dim3(256), 0, st, part, sums, npix, nchunks, W,
-                       H, tile_stride, tile_offset);
+hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, int W, int H, hipStream_t st) {
+    if (WP.n_tail == 0) return hipSuccess;
+    hipLaunchKernelGGL(reduce_chunks_kernel, dim3((WP.n_tail * 64 + 255) / 256), dim3(256), 0, st, part, sums, WP, W,
+                       H);
     return hipGetLastError();
 }
 

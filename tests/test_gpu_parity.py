@@ -82,10 +82,7 @@ def test_hip_matches_live_reference(scene, w, h, spp, ap, fl, seed):
 def test_generic_instantiation_matches(monkeypatch, scene, ap, force):
     """The feature-specialised kernel instantiation and the generic ones give
     identical images: 15 = all features compiled in (affine), 31 = all features
-    with the literal double4 w-lane arithmetic (the path for non-affine scenes).
-    Segment stealing off: with it, a pixel's sum is a sum of segment sums whose
-    boundaries follow each instantiation's own wave schedule."""
-    monkeypatch.setenv("PTMI_NO_STEAL", "1")
+    with the literal double4 w-lane arithmetic (the path for non-affine scenes)."""
     w, h, spp = 40, 24, 3
     objs, tris, grps, cam = scene_inputs(scene, w, h, ap, 1.6 if ap else 0.0)
     seeds = layout.seeds_go_float64(w * h, 77)
@@ -99,9 +96,7 @@ def test_generic_instantiation_matches(monkeypatch, scene, ap, force):
 def test_affine_cores_match_generic_large(monkeypatch, scene, ap):
     """The affine instantiations' divide / sqrt / rsqrt cores (csrc/ptmi_fp64core.h)
     against the generic instantiation's full compiler expansions over a larger
-    frame: 160x120 at 24 spp (~1.8 M paths), images bit-identical (segment stealing
-    off, as in test_generic_instantiation_matches)."""
-    monkeypatch.setenv("PTMI_NO_STEAL", "1")
+    frame: 160x120 at 24 spp (~1.8 M paths), images bit-identical."""
     w, h, spp = 160, 120, 24
     objs, tris, grps, cam = scene_inputs(scene, w, h, ap, 1.6 if ap else 0.0)
     seeds = layout.seeds_go_float64(w * h, 91)
@@ -202,6 +197,29 @@ def test_sample_split_and_chunking_invariance():
     assert (chunked - full).abs().max().item() < 1e-12
 
 
+@pytest.mark.parametrize("scene,stride", [("reference", 1), ("reference", 3), ("teapot", 1), ("teapot", 2)])
+def test_whole_tiles_and_chunked_tail(monkeypatch, scene, stride):
+    """Automatic work plan (ptmi_device.h WorkPlan): whole-tile items first, the last
+    tiles in sample chunks.  PTMI_TAIL_TILES shrinks the chunked tail so a small frame
+    has both kinds; the frame equals the all-whole render (chunks=1) and each tile-split
+    part is zero outside its tiles."""
+    monkeypatch.setenv("PTMI_TAIL_TILES", "5")
+    torch, sc = _torch_scene(scene, 72, 40)
+    S, n = 70, 72 * 40  # 45 tiles (the last column and row partial)
+    seeds = torch.tensor(layout.seeds_go_float64(n, 11), dtype=torch.float64, device="cuda")
+    whole = torch.empty(n * 4, dtype=torch.float64, device="cuda")
+    sc.render(S, 0, S, seeds.data_ptr(), whole.data_ptr(), chunks=1)
+    acc = torch.zeros_like(whole)
+    part = torch.empty_like(whole)
+    for g in range(stride):
+        sc.render(S, 0, S, seeds.data_ptr(), part.data_ptr(), tile_stride=stride, tile_offset=g)
+        acc += part
+    torch.cuda.synchronize()
+    assert torch.all(acc[3::4] == S)
+    assert (acc - whole).abs().max().item() < 1e-12
+    assert torch.all(torch.isfinite(acc))
+
+
 def test_tile_split_partitions_frame():
     torch, sc = _torch_scene("teapot", 40, 24)
     S, n = 3, 40 * 24
@@ -285,21 +303,3 @@ def test_trace_multi_matches_single_device(scene, w, h, spp, split, ndev):
     else:
         assert np.abs(out - single).max() < 1e-12
     assert all(timing[k] >= 0 for k in timing) and timing["total_ms"] >= timing["render_ms"]
-
-
-@pytest.mark.parametrize("scene,w,h,spp", [("teapot", 96, 64, 40), ("gopher", 80, 64, 40),
-                                           ("transparent_teapot", 64, 48, 24)])
-def test_segment_stealing_matches_per_lane_order(monkeypatch, scene, w, h, spp):
-    """BVH scenes: finished lanes take over samples of busy lanes (trace_kernel's
-    segment stealing).  Every path is the same; only the grouping of a pixel's
-    sample sums changes, so the image equals the per-lane order (PTMI_NO_STEAL=1)
-    to FP64 summation rounding, and repeated runs are bit-identical."""
-    objs, tris, grps, cam = scene_inputs(scene, w, h)
-    seeds = layout.seeds_go_float64(w * h, 313)
-    a = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
-    b = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
-    monkeypatch.setenv("PTMI_NO_STEAL", "1")
-    c = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
-    assert np.array_equal(a, b)
-    assert np.abs(a - c).max() < 1e-13
-    assert not np.array_equal(a, c)  # stealing did regroup some sums
