@@ -18,13 +18,16 @@ and rank 0 normalises the frame on device (colors * 1/S, alpha 1;
 tracer.cl:1184-1187).  Total work per step is fixed ("scaling": "strong");
 value = W*H*S*K / (max over ranks of the K-step wall time).
 
-roofline: trace_kernel is FP64-VALU bound (the scene is 8 KB and HBM traffic is
-~0.02 B/sample).  achieved = algorithmic FP64 flops per launch (frozen model,
-profiles/alg_counts.json, ptmi/flops.py) / the kernel's average launch time,
-measured with HIP events recorded on the launch stream around every launch in
-the timed region.  peak = MI355X FP64 vector peak (78.6 TFLOP/s).  `traffic` is
-null: HBM bytes come from rocprofv3 PMC passes, which cannot run inside this
-process (profiles/<round>/ holds them).
+roofline: C2/C3 trace_kernel is FP64-VALU bound (the scene is 8 KB and HBM
+traffic is ~0.02 B/sample): achieved = algorithmic FP64 flops per launch (frozen
+model, profiles/alg_counts.json, ptmi/flops.py) / the kernel's average launch
+time, measured with HIP events recorded on the launch stream around every launch
+in the timed region; peak = MI355X FP64 vector peak (78.6 TFLOP/s).  C4/C5 (BVH
+scenes) report the memory-hierarchy roofline of SURVEY.md 8d: bytes per sample of
+the traversal the kernel runs (tools/traversal_bytes.py) over the 8 TB/s HBM
+peak, with the reference visit rules' bytes and the FP64 figure beside it.
+`traffic` is null: HBM bytes come from rocprofv3 PMC passes, which cannot run
+inside this process (profiles/<round>/ holds them).
 cpu_baseline: the oracle's C restatement of the reference kernel (OpenMP) timed on
 the host cores on a bounded sample of the same frame spread over its sample
 indices, plus the whole C1 frame (rank 0, N=1 only).
@@ -98,6 +101,33 @@ def _cpu_model():
     return "unknown"
 
 
+def host_cpus():
+    """(threads to use, details): the CPUs this process may run on -- its affinity
+    mask, capped by a cgroup v2 CPU quota (cpu.max) when one is set and by the
+    OpenMP thread count the environment grants.  The GPU box grants one GPU's job a
+    16-CPU share of the host (its OMP_NUM_THREADS; jobs there must size worker pools
+    to it), so the baseline runs on that share and reports the machine's nproc and
+    CPU model beside it."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    if omp:
+        cores = min(cores, omp)
+    return cores, {"nproc": nproc, "affinity_cpus": aff, "cgroup_cpu_quota": quota, "omp_num_threads": omp}
+
+
 def cpu_baseline(layout, objs, tris, grps, cam, spp, seeds, budget_s=15.0):
     """The CPU restatement of the reference kernel on the host cores (rank 0, N=1):
     (1) the workload's frame at a bounded sample: every pixel, 8 windows of sample
@@ -110,10 +140,7 @@ def cpu_baseline(layout, objs, tris, grps, cam, spp, seeds, budget_s=15.0):
     from tests.scene_inputs import scene_inputs
     if not pyoracle.cpu_available():
         return None
-    # The GPU box gives one GPU's job a 16-core CPU share (its OMP_NUM_THREADS); os.cpu_count()
-    # there counts the whole machine.  Use what the environment grants, all cores elsewhere.
-    nproc = os.cpu_count() or 1
-    threads = min(nproc, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or nproc)
+    threads, cpus = host_cpus()
     w = int(np.asarray(cam).reshape(())["width"])
     h = int(np.asarray(cam).reshape(())["height"])
     t2, g2 = layout.pad_empty(tris, grps)
@@ -137,7 +164,7 @@ def cpu_baseline(layout, objs, tris, grps, cam, spp, seeds, budget_s=15.0):
             break
         per_win = int(max(1, min(spp // windows, per_win * budget_s / max(el, 1e-3))))
     out = {"value": round(w * h * per_win * windows / el / 1e6, 3), "unit": "Msamples/s", "cores": threads,
-           "nproc": nproc, "cpu_model": _cpu_model(), "kind": "port",
+           "cpus": cpus, "cpu_model": _cpu_model(), "kind": "port",
            "sample": "all %dx%d pixels x samples [k*%d/8, k*%d/8 + %d) for k = 0..7 of the %d-spp frame (%.1f s)"
                      % (w, h, spp, spp, per_win, spp, el),
            "calibration_vs_reference_x86": None,
@@ -270,20 +297,34 @@ def main():
                 ac = json.load(f)["workloads"][alg_key]
             f64 = ac["fp64_flops_per_sample"]
             my_samples_per_launch = npix * (s1 - s0) if split == "sample" else W * H * S / max(world, 1)
-            achieved = f64 * my_samples_per_launch / (avg_ms * 1e-3) / 1e12
-            roof = {"bound": "valu_fp64",
+            rate = my_samples_per_launch / (avg_ms * 1e-3)  # samples/s of the kernel, rank 0
+            achieved = f64 * rate / 1e12
+            fp64 = {"bound": "valu_fp64",
                     "bound_detail": "FP64 vector ALU issue (no MFMA-shaped work; HBM ~0.02 B/sample)",
                     "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": None,
-                    "traffic_note": "HBM bytes per launch from rocprofv3 PMC passes: profiles/r2/SUMMARY.md",
-                    "kernel": "trace_kernel (rank 0)", "kernel_ms_avg": round(avg_ms, 3), "launches": klaunch,
-                    "fp64_flops_per_sample": round(f64, 1),
+                    "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "fp64_flops_per_sample": round(f64, 1),
                     "flops_basis": "reference-rule algorithmic count (oracle -DPTO_COUNT), not executed"}
-            if ac.get("bytes_per_sample"):
-                gbs = ac["bytes_per_sample"] * my_samples_per_launch / (avg_ms * 1e-3) / 1e9
-                roof["memory"] = {"bytes_per_sample": round(ac["bytes_per_sample"], 1), "achieved_GBs": round(gbs, 1),
-                                  "peak_GBs": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                  "basis": "reference visit rules (SURVEY.md 8d B_alg)"}
+            tv = ac.get("traversal")
+            if tv is None:  # C2 / C3: FP64-VALU bound
+                roof = dict(fp64)
+            else:  # C4 / C5: memory hierarchy, bytes of the traversal actually run
+                gbs = tv["bytes_per_sample"] * rate / 1e9
+                ref_gbs = ac["bytes_per_sample"] * rate / 1e9
+                roof = {"bound": "hbm",
+                        "bound_detail": "memory hierarchy (SURVEY.md 8d): BVH node and triangle fetches; the "
+                                        "working set (~1-2 MB) is L2-resident, so the walk is load-latency bound",
+                        "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 4),
+                        "bytes_per_sample": round(tv["bytes_per_sample"], 1), "bytes_basis": tv["basis"],
+                        "reference_rule": {"bytes_per_sample": round(ac["bytes_per_sample"], 1),
+                                           "equivalent_GBs": round(ref_gbs, 1),
+                                           "basis": "the reference's visit rules (tracer.cl:617-719: every "
+                                                    "triangle of every node whose box the line passes): the "
+                                                    "bytes its traversal would fetch at this sample rate"},
+                        "fp64_reference_equivalent": fp64}
+            roof.update({"traffic": None,
+                         "traffic_note": "HBM bytes per launch from rocprofv3 PMC passes (profiles/<round>/)",
+                         "kernel": "trace_kernel (rank 0)", "kernel_ms_avg": round(avg_ms, 3), "launches": klaunch})
         except (OSError, KeyError) as e:
             roof = {"error": "alg counts unavailable: %s" % e}
         cpu = None
