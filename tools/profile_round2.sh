@@ -23,4 +23,5 @@ for c in c2 c4; do
 done
 timeout -k 10 600 bash tools/pmc.sh $OUT/pmc_valu_c2 --config c2 --steps 1 --warmup 0 --no-cpu-baseline --no-trace-call
 timeout -k 10 600 bash tools/pmc.sh $OUT/pmc_valu_c4 --config c4 --steps 1 --warmup 0 --no-cpu-baseline --no-trace-call
+timeout -k 10 600 bash tools/pmc.sh $OUT/pmc_valu_c5 --config c5 --steps 1 --warmup 0 --no-cpu-baseline --no-trace-call
 find $OUT -name "*kernel_stats.csv" | sort
