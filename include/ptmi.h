@@ -110,7 +110,7 @@ typedef struct ptmi_multi_timing {
     double render_ms;   /* until the slowest device has its partial frame: upload, seeds, kernels */
     double combine_ms;  /* from then: xGMI peer copies into the first device + the ordered sum */
     double readback_ms; /* the RGBA frame to host memory */
-    double total_ms;
+    double total_ms;    /* the whole call, releasing the device buffers included */
 } ptmi_multi_timing;
 
 /* ptmi_trace_multi, also reporting its phases in *timing (may be NULL). */

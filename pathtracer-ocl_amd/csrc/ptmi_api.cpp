@@ -784,13 +784,19 @@ extern "C" int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const
     std::vector<int> rcs(n_devices, PTMI_OK);
     std::vector<std::string> msgs(n_devices);
     std::vector<clk::time_point> t_rendered(n_devices, t_prep);
+    // Per-device resources, released after the combine and read-back (hipFree
+    // synchronises; freeing inside the device threads delayed the combine).
+    std::vector<ptmi_scene*> scenes(n_devices, nullptr);
+    std::vector<double*> seeds_d(n_devices, nullptr), sums_d(n_devices, nullptr);
+    std::vector<hipStream_t> streams(n_devices, nullptr);
     auto shard = [&](uint32_t d) {
         char e[512] = {0};
         int& drc = rcs[d];
         const int dev = devices[d];
-        ptmi_scene* s = nullptr;
-        double *d_seeds = nullptr, *d_sums = nullptr;
-        hipStream_t st = nullptr;
+        ptmi_scene*& s = scenes[d];
+        double*& d_seeds = seeds_d[d];
+        double*& d_sums = sums_d[d];
+        hipStream_t& st = streams[d];
         drc = upload_scene(hs, dev, textures, &s, e, sizeof(e));
         if (!drc && dev != root) {  // direct xGMI access to the gather buffer where the link allows it
             int can = 0;
@@ -828,19 +834,25 @@ extern "C" int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const
             drc = PTMI_ERR_HIP;
             std::snprintf(e, sizeof(e), "device %d: peer copy to device %d failed", dev, root);
         }
-        if (st) (void)hipStreamDestroy(st);
-        if (d_seeds) (void)hipFree(d_seeds);
-        if (d_sums) (void)hipFree(d_sums);
-        if (s) ptmi_scene_destroy(s);
         msgs[d] = e;
+    };
+    auto release = [&]() {
+        for (uint32_t d = 0; d < n_devices; d++) {
+            (void)hipSetDevice(devices[d]);
+            if (streams[d]) (void)hipStreamDestroy(streams[d]);
+            if (seeds_d[d]) (void)hipFree(seeds_d[d]);
+            if (sums_d[d]) (void)hipFree(sums_d[d]);
+            if (scenes[d]) ptmi_scene_destroy(scenes[d]);
+        }
+        (void)hipSetDevice(root);
+        (void)hipFree(gather);
     };
     std::vector<std::thread> threads;
     for (uint32_t d = 0; d < n_devices; d++) threads.emplace_back(shard, d);
     for (auto& t : threads) t.join();
     for (uint32_t d = 0; d < n_devices; d++)
         if (rcs[d]) {
-            (void)hipSetDevice(root);
-            (void)hipFree(gather);
+            release();
             set_err(err, err_len, "device %d: %s", devices[d], msgs[d].empty() ? "render failed" : msgs[d].c_str());
             return rcs[d];
         }
@@ -852,7 +864,8 @@ extern "C" int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const
     const clk::time_point t_combined = clk::now();
     if (he == hipSuccess) he = hipMemcpy(out_rgba, frame, frame_bytes, hipMemcpyDeviceToHost);
     const clk::time_point t_end = clk::now();
-    (void)hipFree(gather);
+    release();
+    const clk::time_point t_done = clk::now();
     if (he != hipSuccess) {
         set_err(err, err_len, "combine / read-back on device %d: %s", root, hipGetErrorString(he));
         return PTMI_ERR_HIP;
@@ -862,7 +875,7 @@ extern "C" int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const
         timing->render_ms = ms_since(t_prep, t_all_rendered);
         timing->combine_ms = ms_since(t_all_rendered, t_combined);
         timing->readback_ms = ms_since(t_combined, t_end);
-        timing->total_ms = ms_since(t_start, t_end);
+        timing->total_ms = ms_since(t_start, t_done);
     }
     return PTMI_OK;
 }
