@@ -361,7 +361,9 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
                 }
                 nd.child[i] = 0;  // patched after emit (emit may grow out.nodes)
             } else {
-                for (int k = 0; k < 3; k++) nd.mn[k][i] = nd.mx[k][i] = 0.0f;
+                // an empty slot: a point box at 1e30, culled by the kernel's slab test for
+                // every ray within its pruning limit (ptmi_kernels.hip node_visit)
+                for (int k = 0; k < 3; k++) nd.mn[k][i] = nd.mx[k][i] = 1e30f;
                 nd.child[i] = kEmptyChild;
             }
         }

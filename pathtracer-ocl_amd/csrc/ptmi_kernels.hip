@@ -494,9 +494,17 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 
     }
 }
 
+#ifndef PTMI_NV_FOLD
+#define PTMI_NV_FOLD 1
+#endif
+#ifndef PTMI_NV_BRANCHLESS
+#define PTMI_NV_BRANCHLESS 1  // 2048 spp: C4 798 -> 778, C5 1250 -> 1216 ms (no exec-mask branches per child)
+#endif
 static constexpr int kStack = 24;  // per-lane LDS traversal stack (3 pushes x BVH4 depth <= 7, ptmi_bvh.cpp)
 #ifndef PTMI_LDS_NODES
-#define PTMI_LDS_NODES 21  // Node4s staged in LDS per workgroup: the top 3 BVH4 levels (2.3 KB)
+#define PTMI_LDS_NODES 0  // Node4s staged in LDS per workgroup (the top levels of the index).  0: none --
+                          // every node is a global load (no flat-address select): 2048 spp, C4 808 -> 796,
+                          // C5 1273 -> 1252 ms against 21 (the top 3 levels, 2.3 KB); 1 and 5 in between
 #endif
 static constexpr int kLdsNodes = PTMI_LDS_NODES;
 
@@ -608,11 +616,27 @@ __device__ __forceinline__ bool node_visit(const DevScene& S, const Node4* lds_n
         const float ax = fmaf(mnx[i], rf[0], -ofr[0]), bx = fmaf(mxx[i], rf[0], -ofr[0]);
         const float ay = fmaf(mny[i], rf[1], -ofr[1]), by = fmaf(mxy[i], rf[1], -ofr[1]);
         const float az = fmaf(mnz[i], rf[2], -ofr[2]), bz = fmaf(mxz[i], rf[2], -ofr[2]);
+#if PTMI_NV_FOLD
+        // Entry clamped at 0 and exit clamped at the pruning limit, so one compare
+        // culls a box that is behind the origin (tf < 0), beyond the best hit
+        // (tn > lim) or missed (tn > tf).  NaN bounds (a NaN ray) drop out of the
+        // fmaxf / fminf chains: such a child is entered.  Empty slots hold a point box
+        // at 1e30 (ptmi_bvh.cpp) that no ray within the limit reaches; entering one
+        // would be harmless (kEmptyChild is neither node nor leaf).
+        const float tn = fmaxf(fmaxf(fmaxf(fminf(ax, bx) - dt[0], fminf(ay, by) - dt[1]), fminf(az, bz) - dt[2]), 0.0f);
+        const float tf = fminf(fminf(fminf(fmaxf(ax, bx) + dt[0], fmaxf(ay, by) + dt[1]), fmaxf(az, bz) + dt[2]), lim);
+        k[i] = tn > tf ? __builtin_huge_valf() : tn;
+#else
         const float tn = fmaxf(fmaxf(fminf(ax, bx) - dt[0], fminf(ay, by) - dt[1]), fminf(az, bz) - dt[2]);
         const float tf = fminf(fminf(fmaxf(ax, bx) + dt[0], fmaxf(ay, by) + dt[1]), fmaxf(az, bz) + dt[2]);
         // (NaN bounds -- a NaN ray -- fail every test: the child is entered.)
+#if PTMI_NV_BRANCHLESS
+        const bool cull = (tn > tf) | (tn > lim) | (tf < 0.0f) | (c[i] == kEmptyChild);
+#else
         const bool cull = tn > tf || tn > lim || tf < 0.0f || c[i] == kEmptyChild;
+#endif
         k[i] = cull ? __builtin_huge_valf() : fmaxf(tn, -__builtin_huge_valf());  // NaN -> -inf
+#endif
     }
     // sort (k, c) ascending: 5 compare-exchanges
 #define PTMI_CX(a, b)                                      \
@@ -626,9 +650,20 @@ __device__ __forceinline__ bool node_visit(const DevScene& S, const Node4* lds_n
     }
     PTMI_CX(0, 1) PTMI_CX(2, 3) PTMI_CX(0, 2) PTMI_CX(1, 3) PTMI_CX(1, 2)
 #undef PTMI_CX
+#if PTMI_NV_BRANCHLESS
+    // unconditional stores above the top, the top advanced by the hit flags (sp <= 21
+    // before a node, so the stores stay inside the 24 entries)
+    stk[sp * kStkStride] = c[3];
+    sp += k[3] < __builtin_huge_valf() ? 1 : 0;
+    stk[sp * kStkStride] = c[2];
+    sp += k[2] < __builtin_huge_valf() ? 1 : 0;
+    stk[sp * kStkStride] = c[1];
+    sp += k[1] < __builtin_huge_valf() ? 1 : 0;
+#else
     if (k[3] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[3];
     if (k[2] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[2];
     if (k[1] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[1];
+#endif
     next = c[0];
     return k[0] < __builtin_huge_valf();
 }
