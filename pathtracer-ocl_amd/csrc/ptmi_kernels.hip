@@ -306,7 +306,9 @@ struct Hit {
                 // slot in DevScene::objs (type-run order); -1 = no hit.  One select per
                 // candidate instead of two, and key order is pk order (keys are distinct).
     int tri;    // reference triangle index, -1 for other shapes
-    int chain;  // the triangle's gate-chain code (DevTri::chain)
+    int ti;     // a winning triangle's leaf-order index (DevScene::tris): its gate chain and
+                // barycentrics are re-derived from it after the walks, so they are not
+                // carried through the traversal loop (registers)
     double u, v;
 };
 
@@ -439,8 +441,8 @@ __device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o,
 __device__ __forceinline__ bool chain_certified(const DevScene& S, int chain, d4 o, d4 d, double t);
 
 template <bool kVerify>
-__device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 o, d4 d, int slot, int key, Hit& h,
-                                         int& vchain) {
+__device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, int ti, d4 o, d4 d, int slot, int key,
+                                         Hit& h, int& vchain) {
     const double e1x = T.e1[0], e1y = T.e1[1], e1z = T.e1[2];
     const double e2x = T.e2[0], e2y = T.e2[1], e2z = T.e2[2];
     // dirCrossE2 = cross(d, e2)
@@ -485,13 +487,32 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, d4 
             }
             vchain = c;
         }
-        h.chain = c;
+        h.ti = ti;
         h.t = t;
         h.pk = pack_hit(slot, key);
         h.tri = n;
-        h.u = u;
-        h.v = v;
     }
+}
+
+// The barycentrics of tri_test's hit, re-derived with its operations (bit-identical).
+__device__ __forceinline__ void tri_uv(const DevTri& T, d4 o, d4 d, double& u, double& v) {
+    const double e1x = T.e1[0], e1y = T.e1[1], e1z = T.e1[2];
+    const double e2x = T.e2[0], e2y = T.e2[1], e2z = T.e2[2];
+    const double cx = fma(d.y, e2z, e2y * -d.z), cy = fma(d.z, e2x, e2z * -d.x), cz = fma(d.x, e2y, e2x * -d.y);
+    double det = e1x * cx;
+    det = fma(e1y, cy, det);
+    det = fma(e1z, cz, det);
+    const double px = o.x - T.p1[0], py = o.y - T.p1[1], pz = o.z - T.p1[2];
+    double du = px * cx;
+    du = fma(py, cy, du);
+    du = fma(pz, cz, du);
+    const double f = 1.0 / det;
+    u = f * du;
+    const double qx = fma(py, e1z, e1y * -pz), qy = fma(pz, e1x, e1z * -px), qz = fma(px, e1y, e1x * -py);
+    double dv = d.x * qx;
+    dv = fma(d.y, qy, dv);
+    dv = fma(d.z, qz, dv);
+    v = f * dv;
 }
 
 #ifndef PTMI_NV_FOLD
@@ -678,7 +699,7 @@ __device__ __forceinline__ void leaf_visit(const DevScene& S, int code, int slot
     for (int i = first; i < end; i++) {
         PTMI_COUNT(3);
 #if !(defined(PTMI_EXP) && (PTMI_EXP & 4))
-        tri_test<kVerify>(S, S.tris[i], o, d, slot, key, h, vchain);
+        tri_test<kVerify>(S, S.tris[i], i, o, d, slot, key, h, vchain);
 #endif
     }
 }
@@ -1069,7 +1090,7 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restr
         }
         // Tentative walks: certify the gate chain of a winner from this object while
         // its object-space ray is at hand (a later object that takes over re-certifies).
-        if (!kVerify && h.tri >= 0 && hit_obj(h) == j) cert = chain_certified(S, h.chain, o, d, h.t);
+        if (!kVerify && h.tri >= 0 && hit_obj(h) == j) cert = chain_certified(S, S.tris[h.ti].chain, o, d, h.t);
     }
 }
 
@@ -1092,13 +1113,17 @@ __device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__
         const DevObject& ob = S.objs[hit_obj(h)];
         const d4 o = xpt<A>(ob.inv, ob.st, ro);
         const d4 d = xdir<A>(ob.inv, ob.st, rd);
-        if (!verify_chain(S, h.chain, o, d)) {
+        if (!verify_chain(S, S.tris[h.ti].chain, o, d)) {
             PTMI_COUNT(11);  // (stats build: eager re-walks)
             h = h0;
             group_walks_impl<A, true>(S, stk, lds_nodes, ro, rd, h, cert);
         }
     }
 #endif
+    if (h.tri >= 0) {  // the winner's barycentrics (for its interpolated normal)
+        const DevObject& ob = S.objs[hit_obj(h)];
+        tri_uv(S.tris[h.ti], xpt<A>(ob.inv, ob.st, ro), xdir<A>(ob.inv, ob.st, rd), h.u, h.v);
+    }
 }
 
 // schlick (tracer.cl:485-505)
