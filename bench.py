@@ -193,6 +193,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-trace-call", action="store_true", help="skip the PCIe-inclusive ptmi_trace timing")
     ap.add_argument("--save-image", default="")
+    ap.add_argument("--extra", default="auto",
+                    help="other configs timed after the headline at the same GPU count: a comma list, none, or "
+                         "auto (c3,c5 after a default c2 run at full spp)")
+    ap.add_argument("--extra-steps", type=int, default=2)
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -223,110 +227,153 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
     torch.cuda.set_device(device)
-    scene_name, W, H, S, aper, focal, split, alg_key, desc = CONFIGS[args.config]
-    if args.samples:
-        S = args.samples
-    objs, tris, grps, cam = scene_inputs(scene_name, W, H, aper, focal)
-    scene = api.Scene(device, objs, tris, grps, cam)
-    npix = W * H
-    seeds_host = layout.seeds_go_float64(npix, 1234)
-    seeds = torch.tensor(seeds_host, dtype=torch.float64, device="cuda")
-    sums = torch.empty(npix * 4, dtype=torch.float64, device="cuda")
-    img = torch.empty(npix * 4, dtype=torch.float64, device="cuda")
-    stream = torch.cuda.current_stream().cuda_stream
 
-    s0, s1, t_stride, t_off = pdist.shard(rank, world, S, split)
-    red_ev = []
+    def run_config(cfg, steps, warmup, samples=0, chunks=0, save_image=""):
+        """Render `steps` timed frames of config `cfg` on this rank's share (after
+        `warmup` untimed ones): barrier + synchronize on both sides, max over ranks.
+        Returns (per-config results on rank 0, the scene inputs)."""
+        scene_name, W, H, S, aper, focal, split, alg_key, desc = CONFIGS[cfg]
+        if samples:
+            S = samples
+        objs, tris, grps, cam = scene_inputs(scene_name, W, H, aper, focal)
+        scene = api.Scene(device, objs, tris, grps, cam)
+        npix = W * H
+        seeds_host = layout.seeds_go_float64(npix, 1234)
+        seeds = torch.tensor(seeds_host, dtype=torch.float64, device="cuda")
+        sums = torch.empty(npix * 4, dtype=torch.float64, device="cuda")
+        img = torch.empty(npix * 4, dtype=torch.float64, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        s0, s1, t_stride, t_off = pdist.shard(rank, world, S, split)
+        red_ev = []
 
-    def step():
-        scene.render(S, s0, s1, seeds.data_ptr(), sums.data_ptr(), tile_stride=t_stride, tile_offset=t_off,
-                     chunks=args.chunks, stream=stream)
+        def step():
+            scene.render(S, s0, s1, seeds.data_ptr(), sums.data_ptr(), tile_stride=t_stride, tile_offset=t_off,
+                         chunks=chunks, stream=stream)
+            if world > 1:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                pdist.reduce_frame_to(sums, 0, via_host=shared)  # RCCL reduce over xGMI onto rank 0
+                e1.record()
+                red_ev.append((e0, e1))
+            if rank == 0:
+                scene.finalize(sums.data_ptr(), img.data_ptr(), S, stream=stream)
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        scene.kernel_time()  # drop warmup launches
+        red_ev.clear()
+        scene.set_timing(True)
         if world > 1:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            pdist.reduce_frame_to(sums, 0, via_host=shared)  # RCCL reduce over xGMI onto rank 0
-            e1.record()
-            red_ev.append((e0, e1))
-        if rank == 0:
-            scene.finalize(sums.data_ptr(), img.data_ptr(), S, stream=stream)
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        kms, klaunch = scene.kernel_time()
+        scene.set_timing(False)
+        red_ms = sum(a.elapsed_time(b) for a, b in red_ev) / max(len(red_ev), 1)
+        # per-rank [wall, kernel ms per launch, reduce ms] gathered on every rank
+        red_dev = "cpu" if shared else "cuda"
+        mine = torch.zeros(world, 3, dtype=torch.float64, device=red_dev)
+        mine[rank, 0] = el
+        mine[rank, 1] = kms / max(klaunch, 1)
+        mine[rank, 2] = red_ms
+        if world > 1:
+            dist.all_reduce(mine, op=dist.ReduceOp.SUM)
+        per_rank = mine.cpu().numpy()
+        el = float(per_rank[:, 0].max())
+        res = None
+        if rank == 0:  # sanity: a finite image with alpha 1
+            im = img.view(H, W, 4)
+            ok = bool(torch.isfinite(im).all().item()) and bool((im[..., 3] == 1.0).all().item())
+            if save_image:
+                np.save(save_image, im.cpu().numpy())
+            avg_ms = float(per_rank[0, 1])
+            my_samples_per_launch = npix * (s1 - s0) if split == "sample" else W * H * S / max(world, 1)
+            par = "single GPU"
+            if world > 1:
+                par = "%s-split x%d + RCCL reduce" % (split, world) if not shared else \
+                    "%s-split x%d ranks on %d device(s), gloo host reduce (rehearsal)" % (split, world, ndev)
+            res = {"value": W * H * S * steps / el / 1e6, "ms_per_step": el / steps * 1e3, "image_ok": ok,
+                   "avg_kernel_ms": avg_ms, "launches": klaunch, "per_rank": per_rank,
+                   "rate": my_samples_per_launch / (avg_ms * 1e-3), "alg_key": alg_key, "split": split,
+                   "config": {"workload": desc, "scene": scene_name, "width": W, "height": H, "spp": S,
+                              "aperture": aper, "focal_length": focal, "split": split, "parallelism": par}}
+        scene.close()
+        del seeds, sums, img
+        return res, (objs, tris, grps, cam, S, seeds_host)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    scene.kernel_time()  # drop warmup launches
-    red_ev.clear()
-    scene.set_timing(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    kms, klaunch = scene.kernel_time()
-    scene.set_timing(False)
-    red_ms = sum(a.elapsed_time(b) for a, b in red_ev) / max(len(red_ev), 1)
-    # per-rank [wall, kernel ms per launch, reduce ms] gathered on every rank
-    red_dev = "cpu" if shared else "cuda"
-    mine = torch.zeros(world, 3, dtype=torch.float64, device=red_dev)
-    mine[rank, 0] = el
-    mine[rank, 1] = kms / max(klaunch, 1)
-    mine[rank, 2] = red_ms
-    if world > 1:
-        dist.all_reduce(mine, op=dist.ReduceOp.SUM)
-    per_rank = mine.cpu().numpy()
-    el = float(per_rank[:, 0].max())
-
-    ok = True
-    if rank == 0:  # sanity: a finite image with alpha 1
-        im = img.view(H, W, 4)
-        ok = bool(torch.isfinite(im).all().item()) and bool((im[..., 3] == 1.0).all().item())
-        if args.save_image:
-            np.save(args.save_image, im.cpu().numpy())
-
-    if rank == 0:
-        total = W * H * S * args.steps
-        value = total / el / 1e6
-        avg_ms = float(per_rank[0, 1])
-        roof = None
+    def roofline(res):
+        """The dominant kernel's roofline for one config's result (rank 0)."""
         try:
             with open(os.path.join(ROOT, "profiles", "alg_counts.json")) as f:
-                ac = json.load(f)["workloads"][alg_key]
-            f64 = ac["fp64_flops_per_sample"]
-            my_samples_per_launch = npix * (s1 - s0) if split == "sample" else W * H * S / max(world, 1)
-            rate = my_samples_per_launch / (avg_ms * 1e-3)  # samples/s of the kernel, rank 0
-            achieved = f64 * rate / 1e12
-            fp64 = {"bound": "valu_fp64",
-                    "bound_detail": "FP64 vector ALU issue (no MFMA-shaped work; HBM ~0.02 B/sample)",
-                    "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "fp64_flops_per_sample": round(f64, 1),
-                    "flops_basis": "reference-rule algorithmic count (oracle -DPTO_COUNT), not executed"}
-            tv = ac.get("traversal")
-            if tv is None:  # C2 / C3: FP64-VALU bound
-                roof = dict(fp64)
-            else:  # C4 / C5: memory hierarchy, bytes of the traversal actually run
-                gbs = tv["bytes_per_sample"] * rate / 1e9
-                ref_gbs = ac["bytes_per_sample"] * rate / 1e9
-                roof = {"bound": "hbm",
-                        "bound_detail": "memory hierarchy (SURVEY.md 8d): BVH node and triangle fetches; the "
-                                        "working set (~1-2 MB) is L2-resident, so the walk is load-latency bound",
-                        "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(gbs / HBM_PEAK_GBS, 4),
-                        "bytes_per_sample": round(tv["bytes_per_sample"], 1), "bytes_basis": tv["basis"],
-                        "reference_rule": {"bytes_per_sample": round(ac["bytes_per_sample"], 1),
-                                           "equivalent_GBs": round(ref_gbs, 1),
-                                           "basis": "the reference's visit rules (tracer.cl:617-719: every "
-                                                    "triangle of every node whose box the line passes): the "
-                                                    "bytes its traversal would fetch at this sample rate"},
-                        "fp64_reference_equivalent": fp64}
-            roof.update({"traffic": None,
-                         "traffic_note": "HBM bytes per launch from rocprofv3 PMC passes (profiles/<round>/)",
-                         "kernel": "trace_kernel (rank 0)", "kernel_ms_avg": round(avg_ms, 3), "launches": klaunch})
+                ac = json.load(f)["workloads"][res["alg_key"]]
         except (OSError, KeyError) as e:
-            roof = {"error": "alg counts unavailable: %s" % e}
+            return {"error": "alg counts unavailable: %s" % e}
+        rate = res["rate"]  # samples/s of the kernel, rank 0
+        f64 = ac["fp64_flops_per_sample"]
+        achieved = f64 * rate / 1e12
+        fp64 = {"bound": "valu_fp64",
+                "bound_detail": "FP64 vector ALU issue (no MFMA-shaped work; HBM ~0.02 B/sample)",
+                "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "fp64_flops_per_sample": round(f64, 1),
+                "flops_basis": "reference-rule algorithmic count (oracle -DPTO_COUNT), not executed"}
+        tv = ac.get("traversal")
+        if tv is None:  # C2 / C3: FP64-VALU bound
+            roof = dict(fp64)
+        else:  # C4 / C5: memory hierarchy (SURVEY.md 8d), bytes of the traversal actually run
+            gbs = tv["bytes_per_sample"] * rate / 1e9
+            ref_gbs = ac["bytes_per_sample"] * rate / 1e9
+            roof = {"bound": "hbm",
+                    "bound_detail": "memory hierarchy (SURVEY.md 8d): BVH node and triangle fetches; the "
+                                    "working set (~1-2 MB) is L2-resident, so the walk is load-latency bound",
+                    "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(gbs / HBM_PEAK_GBS, 4),
+                    "bytes_per_sample": round(tv["bytes_per_sample"], 1), "bytes_basis": tv["basis"],
+                    "reference_rule": {"bytes_per_sample": round(ac["bytes_per_sample"], 1),
+                                       "equivalent_GBs": round(ref_gbs, 1),
+                                       "basis": "the reference's visit rules (tracer.cl:617-719: every "
+                                                "triangle of every node whose box the line passes): the "
+                                                "bytes its traversal would fetch at this sample rate"},
+                    "fp64_reference_equivalent": fp64}
+        roof.update({"traffic": None,
+                     "traffic_note": "HBM bytes per launch from rocprofv3 PMC passes (profiles/<round>/)",
+                     "kernel": "trace_kernel (rank 0)", "kernel_ms_avg": round(res["avg_kernel_ms"], 3),
+                     "launches": res["launches"]})
+        return roof
+
+    res, (objs, tris, grps, cam, S, seeds_host) = run_config(args.config, args.steps, args.warmup, args.samples,
+                                                             args.chunks, args.save_image)
+    # The other BASELINE configurations at this GPU count, after the headline frames
+    # (C3 / C5 are the reference's 8-GPU configurations; the driver's 1/2/4/8 runs then
+    # measure their scaling too).  Secondary: `value` and `ms_per_step` are the headline's.
+    extras = {}
+    extra = args.extra
+    if extra == "auto":
+        extra = "c3,c5" if args.config == "c2" and not args.samples and not args.chunks else "none"
+    for cfg in [c for c in extra.split(",") if c and c != "none" and c != args.config]:
+        r, _ = run_config(cfg, args.extra_steps, 1)
+        if rank == 0:
+            ex = {"value": round(r["value"], 2), "unit": "Msamples/s", "ms_per_step": round(r["ms_per_step"], 3),
+                  "steps": args.extra_steps, "warmup": 1, "image_ok": r["image_ok"], "config": r["config"],
+                  "roofline_frac": roofline(r).get("frac")}
+            if world > 1:
+                ex["per_rank_kernel_ms"] = [round(float(x), 3) for x in r["per_rank"][:, 1]]
+                ex["reduce_ms"] = round(float(r["per_rank"][0, 2]), 3)
+            extras[cfg] = ex
+
+    if rank == 0:
+        scene_name, W, H = res["config"]["scene"], res["config"]["width"], res["config"]["height"]
+        per_rank = res["per_rank"]
+        value = res["value"]
+        ok = res["image_ok"]
+        el = res["ms_per_step"] * args.steps / 1e3
+        roof = roofline(res)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(layout, objs, tris, grps, cam, S, seeds_host)
@@ -343,25 +390,21 @@ def main():
             inclusive = {"ms": round(t_call * 1e3, 3), "value": round(W * H * S / t_call / 1e6, 2),
                          "unit": "Msamples/s", "what": "one ptmi_trace call: records + seeds from host memory, "
                                                        "scene upload and BVH build, kernels, RGBA read-back"}
-        par = "single GPU"
-        if world > 1:
-            par = "%s-split x%d + RCCL reduce" % (split, world) if not shared else \
-                "%s-split x%d ranks on %d device(s), gloo host reduce (rehearsal)" % (split, world, ndev)
         line = {
             "metric": "Msamples/sec (1280x960 ref scene)", "value": round(value, 2), "unit": "Msamples/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: restated reference scene records, PCG64 per-pixel seeds",
-            "config": {"workload": desc, "scene": scene_name, "width": W, "height": H, "spp": S,
-                       "aperture": aper, "focal_length": focal, "split": split, "parallelism": par},
+            "config": res["config"],
             "image_ok": ok, "roofline": roof, "cpu_baseline": cpu, "ptmi_trace_call": inclusive,
         }
         if world > 1:
             line["per_rank"] = {"kernel_ms": [round(float(x), 3) for x in per_rank[:, 1]],
                                 "wall_s": [round(float(x), 4) for x in per_rank[:, 0]],
                                 "reduce_ms": round(float(per_rank[0, 2]), 3), "shared_devices": shared}
+        if extras:
+            line["extra_configs"] = extras
         print(json.dumps(line), flush=True)
-    scene.close()
     if world > 1:
         dist.destroy_process_group()
 

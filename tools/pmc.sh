@@ -4,7 +4,7 @@
 #   bash tools/pmc.sh <outdir> [bench args...]
 set -e
 OUT=${1:-gpurun_out/pmc}; shift || true
-ARGS=${@:---steps 1 --warmup 0 --samples 64 --no-cpu-baseline}
+ARGS=${@:---steps 1 --warmup 0 --samples 64 --no-cpu-baseline --extra none}
 export TMPDIR=/tmp
 mkdir -p $OUT
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
