@@ -717,7 +717,14 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
     int sp = 0;
     int cur = R.entry;
     PTMI_COUNT(0);
+#if PTMI_STATS == 1
+    int n_steps = 0, n_leaves = 0;  // (stats: walks that end at the root / without a leaf)
+#endif
     while (true) {
+#if PTMI_STATS == 1
+        n_steps++;
+        n_leaves += (cur < 0 && cur != kEmptyChild) ? 1 : 0;
+#endif
         PTMI_COUNT_ACTIVE(19);  // (stats: wave-level walk loop iterations)
         PTMI_TSTAMP(t_nd);
         if (cur >= 0) {
@@ -736,6 +743,10 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
         if (sp == 0) break;
         cur = stk[(--sp) * kStkStride];
     }
+#if PTMI_STATS == 1
+    if (n_leaves == 0) PTMI_COUNT(20);
+    if (n_steps == 1) PTMI_COUNT(21);
+#endif
 }
 
 // Candidate update as selects (no exec-mask branching).  t > EPSILON implies

@@ -35,3 +35,17 @@ def test_bench_launches_ranks_itself(config):
     assert d["n_gpus"] == 2 and d["image_ok"]
     assert len(d["per_rank"]["kernel_ms"]) == 2 and all(k > 0 for k in d["per_rank"]["kernel_ms"])
     assert d["cpu_baseline"] is None and d["ptmi_trace_call"] is None
+
+
+def test_bench_extra_configs_line():
+    """The other BASELINE configurations timed after the headline at the same GPU count
+    (the default run does c3,c5; here at 2 ranks sharing the device, one timed frame each)."""
+    d = _bench("--gpus", "2", "--samples", "16", "--steps", "1", "--warmup", "0", "--extra", "c3,c5",
+               "--extra-steps", "1")
+    assert d["config"]["scene"] == "reference" and d["n_gpus"] == 2
+    ex = d["extra_configs"]
+    assert sorted(ex) == ["c3", "c5"]
+    assert ex["c3"]["config"]["split"] == "sample" and ex["c5"]["config"]["split"] == "tile"
+    for v in ex.values():
+        assert v["image_ok"] and v["value"] > 0 and len(v["per_rank_kernel_ms"]) == 2
+        assert v["config"]["spp"] == 2048 and v["steps"] == 1
