@@ -100,6 +100,12 @@ static constexpr int kRefillNeed = PTMI_REFILL_NEED;
 #define PTMI_WALK_BATCH 24
 #endif
 static constexpr int kWalkBatch = PTMI_WALK_BATCH;  // parked lanes that trigger a wave's BVH walk phase
+#ifndef PTMI_ACC_LDS
+#define PTMI_ACC_LDS 1  // group scenes: per-pixel colour sums in LDS instead of registers
+#endif
+#ifndef PTMI_HP_LDS
+#define PTMI_HP_LDS 1  // group scenes: a parked lane's primitive best (t, pk) in LDS
+#endif
 #ifndef PTMI_SPHERE_RCP
 #define PTMI_SPHERE_RCP 1  // both sphere roots from one reciprocal (sphere_roots)
 #endif
@@ -1604,6 +1610,15 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
     const float fgi2 = (float)(seed / (double)samples);
     const uint32_t c_end = c1;
     double cr = 0.0, cg = 0.0, cb = 0.0;  // colors (tracer.cl:1179)
+    // Group scenes may keep the sums in LDS (one slot per lane, the same additions in the
+    // same order): they change once per path, and the walk phases need the registers.
+    constexpr bool kAccLds = (FL & F_GROUPS) != 0 && PTMI_ACC_LDS;
+    __shared__ double acc_lds[kAccLds ? 3 * kBlock : 1];
+    if constexpr (kAccLds) {
+        acc_lds[0 * kBlock + threadIdx.x] = 0.0;
+        acc_lds[1 * kBlock + threadIdx.x] = 0.0;
+        acc_lds[2 * kBlock + threadIdx.x] = 0.0;
+    }
     // Camera rays are produced in wave-wide batches into a kCamDepth-deep per-lane
     // ring buffer (LDS) and consumed by path regeneration: generating them at the
     // moment each lane needs one would run the camera block (2 noise3D + the
@@ -1628,6 +1643,9 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
     bool active = false, pending = false;
     PathState P;
     Hit hp;
+    constexpr bool kHpLds = (FL & F_GROUPS) != 0 && PTMI_HP_LDS;
+    __shared__ double hp_t_lds[kHpLds ? kBlock : 1];
+    __shared__ int hp_pk_lds[kHpLds ? kBlock : 1];
     PTMI_TSTAMP(t_loop);
     for (;;) {
         if (!__any(active || nb > 0 || n_gen < c_end)) break;
@@ -1695,7 +1713,12 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
                 h = find_closest_prims<FL>(S, P.ro, P.rd);
                 if ((FL & F_GROUPS) && group_needs_walk<A>(S, P.ro, P.rd, h)) {
                     pending = true;
-                    hp = h;
+                    if constexpr (kHpLds) {  // find_closest_prims: tri, ti, u, v are constants
+                        hp_t_lds[threadIdx.x] = h.t;
+                        hp_pk_lds[threadIdx.x] = h.pk;
+                    } else {
+                        hp = h;
+                    }
                 } else {
                     ready = true;
                 }
@@ -1709,7 +1732,11 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
                 PTMI_WADD(8, 1ull);
                 PTMI_WADD(9, (unsigned long long)n_pend);
                 if (pending) {
-                    h = hp;
+                    if constexpr (kHpLds) {
+                        h = Hit{hp_t_lds[threadIdx.x], hp_pk_lds[threadIdx.x], -1, -1, 0.0, 0.0};
+                    } else {
+                        h = hp;
+                    }
                     group_walks<A>(S, stk, node_lds, P.ro, P.rd, h);
                     pending = false;
                     ready = true;
@@ -1721,9 +1748,16 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
         PTMI_WADD(25, (unsigned long long)__popcll(__ballot(pending)));
         PTMI_TSTAMP(t_d);
         if (ready && bounce_shade<FL>(S, P, h, fgi, n_cur)) {
-            cr = cr + P.ar;  // colors += accumColor (tracer.cl:1179)
-            cg = cg + P.ag;
-            cb = cb + P.ab;
+            if constexpr (kAccLds) {
+                double* a = acc_lds + threadIdx.x;
+                a[0 * kBlock] = a[0 * kBlock] + P.ar;
+                a[1 * kBlock] = a[1 * kBlock] + P.ag;
+                a[2 * kBlock] = a[2 * kBlock] + P.ab;
+            } else {
+                cr = cr + P.ar;  // colors += accumColor (tracer.cl:1179)
+                cg = cg + P.ag;
+                cb = cb + P.ab;
+            }
             active = false;
         }
         PTMI_TADD(15, t_d);
@@ -1734,6 +1768,11 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_
         for (int k = 0; k < 32; k++)
             if (ptmi_wstat[threadIdx.x >> 6][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[threadIdx.x >> 6][k]);
 #endif
+    if constexpr (kAccLds) {
+        cr = acc_lds[0 * kBlock + threadIdx.x];
+        cg = acc_lds[1 * kBlock + threadIdx.x];
+        cb = acc_lds[2 * kBlock + threadIdx.x];
+    }
     double* o = (whole ? sums : part) + oslot * 4;
     o[0] = cr;
     o[1] = cg;
