@@ -55,23 +55,36 @@ __device__ __forceinline__ double rsqrt_core(double x) {  // ocml rsqrt_f64 for 
     return fma(t, e, r);
 }
 
+// The constants of sincos_core (ocml's __ocml_sincos_f64), in order of first use.
+static constexpr uint64_t kSincosBits[17] = {0x3FE45F306DC9C883ull, 0xBFF921FB54442D18ull, 0xBC91A62633145C00ull, 0x3C91A62633145C00ull, 0xB97B839A252049C0ull, 0xBDA907DB46CC5E42ull, 0x3E21EEB69037AB78ull, 0xBE927E4FA17F65F6ull, 0x3EFA01A019F4EC90ull, 0xBF56C16C16C16967ull, 0x3FA5555555555555ull, 0x3DE5E0B2F9A43BB8ull, 0xBE5AE600B42FDFA7ull, 0x3EC71DE3796CDE01ull, 0xBF2A01A019E83E5Cull, 0x3F81111111110BB3ull, 0xBFC5555555555555ull};
+static __constant__ double kSincosK[17] = {__builtin_bit_cast(double, 0x3FE45F306DC9C883ull), __builtin_bit_cast(double, 0xBFF921FB54442D18ull), __builtin_bit_cast(double, 0xBC91A62633145C00ull), __builtin_bit_cast(double, 0x3C91A62633145C00ull), __builtin_bit_cast(double, 0xB97B839A252049C0ull), __builtin_bit_cast(double, 0xBDA907DB46CC5E42ull), __builtin_bit_cast(double, 0x3E21EEB69037AB78ull), __builtin_bit_cast(double, 0xBE927E4FA17F65F6ull), __builtin_bit_cast(double, 0x3EFA01A019F4EC90ull), __builtin_bit_cast(double, 0xBF56C16C16C16967ull), __builtin_bit_cast(double, 0x3FA5555555555555ull), __builtin_bit_cast(double, 0x3DE5E0B2F9A43BB8ull), __builtin_bit_cast(double, 0xBE5AE600B42FDFA7ull), __builtin_bit_cast(double, 0x3EC71DE3796CDE01ull), __builtin_bit_cast(double, 0xBF2A01A019E83E5Cull), __builtin_bit_cast(double, 0x3F81111111110BB3ull), __builtin_bit_cast(double, 0xBFC5555555555555ull)};
+
 // ocml's __ocml_sincos_f64 for 0 <= x < 1024 (ROCm 7.2 ocml.bc, read off the IR):
 // __ocmlpriv_trigredsmall_f64 (Cody-Waite with a double-double remainder), then
 // __ocmlpriv_sincosred2_f64 and the quadrant swap.  Left out, being identities on
 // this domain: the large-argument branch (x >= 2^30), the sign of x (+0), the
 // non-finite fix-up, and the error term fma(k, pio2_m, -k * pio2_m), which is +0
 // because pio2_m has 43 significant bits and k = rint(x * 2/pi) < 2^10.
+template <bool kMem = false>
 __device__ __forceinline__ void sincos_core(double x, double* sp, double* cp) {
-    const double dn = __builtin_rint(x * __builtin_bit_cast(double, 0x3FE45F306DC9C883ull));
-    const double t4 = fma(dn, __builtin_bit_cast(double, 0xBFF921FB54442D18ull), x);
-    const double t5 = fma(dn, __builtin_bit_cast(double, 0xBC91A62633145C00ull), t4);
-    const double t6 = dn * __builtin_bit_cast(double, 0x3C91A62633145C00ull);
+    // kMem: the constants are read from a __constant__ table (scalar loads into SGPRs)
+    // instead of being materialised as literals, which the allocator hoists out of the
+    // bounce loop into ~20 VGPRs (same values, same bits).  The product kernels use the
+    // table: the group kernels then stop spilling, and C2/C3 fit 5 waves per SIMD.
+    auto K = [](int i) -> double {
+        if constexpr (kMem) return kSincosK[i];
+        else return __builtin_bit_cast(double, kSincosBits[i]);
+    };
+    const double dn = __builtin_rint(x * K(0));
+    const double t4 = fma(dn, K(1), x);
+    const double t5 = fma(dn, K(2), t4);
+    const double t6 = dn * K(3);
     const double t9 = t4 - t6;
     const double t10 = t4 - t9;
     const double t11 = t10 - t6;
     const double t12 = t9 - t5;
     const double t13 = t12 + t11;
-    const double t15 = fma(dn, __builtin_bit_cast(double, 0xB97B839A252049C0ull), t13);
+    const double t15 = fma(dn, K(4), t13);
     const double rh = t5 + t15;
     const double rl = t15 - (rh - t5);
     const int q = ((int)dn) & 3;
@@ -81,20 +94,20 @@ __device__ __forceinline__ void sincos_core(double x, double* sp, double* cp) {
     const double c0 = 1.0 - hx;
     const double c1 = (1.0 - c0) - hx;
     const double x4 = x2 * x2;
-    double pc = fma(x2, __builtin_bit_cast(double, 0xBDA907DB46CC5E42ull), __builtin_bit_cast(double, 0x3E21EEB69037AB78ull));
-    pc = fma(x2, pc, __builtin_bit_cast(double, 0xBE927E4FA17F65F6ull));
-    pc = fma(x2, pc, __builtin_bit_cast(double, 0x3EFA01A019F4EC90ull));
-    pc = fma(x2, pc, __builtin_bit_cast(double, 0xBF56C16C16C16967ull));
-    pc = fma(x2, pc, __builtin_bit_cast(double, 0x3FA5555555555555ull));
+    double pc = fma(x2, K(5), K(6));
+    pc = fma(x2, pc, K(7));
+    pc = fma(x2, pc, K(8));
+    pc = fma(x2, pc, K(9));
+    pc = fma(x2, pc, K(10));
     const double cc = c0 + fma(x4, pc, fma(rh, -rl, c1));
-    double ps = fma(x2, __builtin_bit_cast(double, 0x3DE5E0B2F9A43BB8ull), __builtin_bit_cast(double, 0xBE5AE600B42FDFA7ull));
-    ps = fma(x2, ps, __builtin_bit_cast(double, 0x3EC71DE3796CDE01ull));
-    ps = fma(x2, ps, __builtin_bit_cast(double, 0xBF2A01A019E83E5Cull));
-    ps = fma(x2, ps, __builtin_bit_cast(double, 0x3F81111111110BB3ull));
+    double ps = fma(x2, K(11), K(12));
+    ps = fma(x2, ps, K(13));
+    ps = fma(x2, ps, K(14));
+    ps = fma(x2, ps, K(15));
     const double x3 = rh * -x2;
     const double s1 = fma(x3, ps, rl * 0.5);
     const double s2 = fma(x2, s1, -rl);
-    const double ss = rh - fma(x3, __builtin_bit_cast(double, 0xBFC5555555555555ull), s2);
+    const double ss = rh - fma(x3, K(16), s2);
     // __ocml_sincos_f64: quadrant swap and sign flips (x >= 0)
     const uint64_t flip = (q > 1) ? 0x8000000000000000ull : 0ull;
     const double sv = (q & 1) ? cc : ss;

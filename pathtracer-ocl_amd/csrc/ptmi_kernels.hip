@@ -103,6 +103,9 @@ static constexpr int kWalkBatch = PTMI_WALK_BATCH;  // parked lanes that trigger
 #ifndef PTMI_ACC_LDS
 #define PTMI_ACC_LDS 1  // group scenes: per-pixel colour sums in LDS instead of registers
 #endif
+#ifndef PTMI_SINCOS_KMEM
+#define PTMI_SINCOS_KMEM 2  // sincos constants from a __constant__ table (ptmi_fp64core.h): 1 group scenes, 2 all
+#endif
 #ifndef PTMI_HP_LDS
 #define PTMI_HP_LDS 1  // group scenes: a parked lane's primitive best (t, pk) in LDS
 #endif
@@ -1173,7 +1176,7 @@ template <bool A>
 __device__ __forceinline__ d4 reflect(d4 rd, d4 nv) { return sub4(rd, scl4(scl4(nv, 2.0), dotv<A>(rd, nv))); }
 
 // randomVectorInHemisphere (tracer.cl:348-366); x, y, z hold float-valued doubles.
-template <bool A>
+template <bool A, bool kKMem>
 __device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float fz) {
     double rand1 = 2.0 * kPi * (double)noise3d(fx, fy, fz);
     double rand2 = (double)noise3d(fy, fz, fx);
@@ -1192,7 +1195,7 @@ __device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float
         cr = 1.0 - rand1 * 0.1;
         sr = rand1 * 0.15;
     } else if constexpr (A) {
-        sincos_core(rand1, &sr, &cr);  // rand1 in [0, 2 pi): ocml's sincos without its range steps
+        sincos_core<kKMem>(rand1, &sr, &cr);  // rand1 in [0, 2 pi): ocml's sincos without its range steps
     } else {
         sincos(rand1, &sr, &cr);  // ocml sincos == (sin, cos) bit-for-bit: one shared reduction
     }
@@ -1494,7 +1497,8 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
             reflecting = true;
         }
     } else {
-        P.rd = random_hemisphere<A>(nv, fgi, (float)b, (float)n);
+        P.rd = random_hemisphere<A, PTMI_SINCOS_KMEM == 2 || ((FL & F_GROUPS) != 0 && PTMI_SINCOS_KMEM == 1)>(nv, fgi, (float)b,
+                                                                                              (float)n);
         cosine = dotv<A>(P.rd, nv);
     }
     P.ro = over;
@@ -1548,14 +1552,20 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
 // Writes the chunk's RGB sums (A = #samples) to out[(chunk*npix + pixel)*4].
 template <int FL>
 #ifndef PTMI_WAVES
-#define PTMI_WAVES 3        // waves/SIMD the register allocation targets (scenes without groups).  The kernel is
-                            // VALU-issue bound: C2 2048 spp 186.3 ms at 3 (no spill) vs 189.0 at 5 (96 VGPRs +
-                            // 80 B/lane of spilled loop invariants) and 186.3 at 2; C3 flat (196.3 vs 195.9)
+#define PTMI_WAVES 5  // waves/SIMD the register allocation targets (scenes without groups or materials).
+                      // The kernel is VALU-issue bound.  With the sincos constants in SGPRs (ptmi_fp64core.h)
+                      // C2/C3 fit 95 VGPRs without spill: C2 2048 spp 178.0 -> 171.6 ms, C3 185.6 -> 179.6 ms
+                      // against the 3-wave budget (round 1: 5 waves spilled 80 B/lane and lost 1.4 %)
+#endif
+#ifndef PTMI_WAVES_MATERIALS
+#define PTMI_WAVES_MATERIALS 3  // ... with reflective / refractive materials (at 5 they spill 96-112 B/lane)
 #endif
 #ifndef PTMI_WAVES_GROUPS
 #define PTMI_WAVES_GROUPS 3  // ... and with BVH groups (the walk needs more registers; 4 spills)
 #endif
-__global__ __launch_bounds__(kBlock, (FL & F_GROUPS) ? PTMI_WAVES_GROUPS : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, WorkPlan WP,
+__global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
+                                    : (FL & F_MATERIALS) ? PTMI_WAVES_MATERIALS
+                                                         : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, WorkPlan WP,
                                                     const double* __restrict__ seeds, const double* __restrict__ sunf,
                                                     double* __restrict__ sums, double* __restrict__ part) {
     // Top levels of the traversal index in LDS (group scenes), staged by the whole

@@ -100,7 +100,7 @@ __global__ void fp64core_check(uint64_t seed, uint64_t per_thread, unsigned long
     if (m2) atomicAdd(&mism[2], m2);
 }
 
-// ptmi::sincos_core against ocml's sincos for the hemisphere angle of every noise
+// ptmi::sincos_core (both constant sources) against ocml's sincos for the hemisphere angle of every noise
 // value: rand1 = 2 * (double)3.14159265359f * (double)v for each float v in [0, 1)
 // (tracer.cl:349, as ptmi_kernels.hip random_hemisphere computes it).
 __global__ void sincos_check(unsigned long long* mism, unsigned int* first) {
@@ -108,10 +108,12 @@ __global__ void sincos_check(unsigned long long* mism, unsigned int* first) {
     if (bits >= 0x3F800000u) return;
     const double kpi = (double)3.14159265359f;
     const double x = 2.0 * kpi * (double)pto_bits2f(bits);
-    double s0, c0, s1, c1;
+    double s0, c0, s1, c1, s2, c2;
     sincos(x, &s0, &c0);
     ptmi::sincos_core(x, &s1, &c1);
-    if (__double_as_longlong(s0) != __double_as_longlong(s1) || __double_as_longlong(c0) != __double_as_longlong(c1)) {
+    ptmi::sincos_core<true>(x, &s2, &c2);  // constants from the __constant__ table (group kernels)
+    if (__double_as_longlong(s0) != __double_as_longlong(s1) || __double_as_longlong(c0) != __double_as_longlong(c1) ||
+        __double_as_longlong(s0) != __double_as_longlong(s2) || __double_as_longlong(c0) != __double_as_longlong(c2)) {
         atomicAdd(mism, 1ull);
         atomicMin(first, bits);
     }
