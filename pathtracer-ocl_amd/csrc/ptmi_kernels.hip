@@ -1552,10 +1552,12 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
 // Writes the chunk's RGB sums (A = #samples) to out[(chunk*npix + pixel)*4].
 template <int FL>
 #ifndef PTMI_WAVES
-#define PTMI_WAVES 5  // waves/SIMD the register allocation targets (scenes without groups or materials).
+#define PTMI_WAVES 6  // waves/SIMD the register allocation targets (scenes without groups or materials).
                       // The kernel is VALU-issue bound.  With the sincos constants in SGPRs (ptmi_fp64core.h)
-                      // C2/C3 fit 95 VGPRs without spill: C2 2048 spp 178.0 -> 171.6 ms, C3 185.6 -> 179.6 ms
-                      // against the 3-wave budget (round 1: 5 waves spilled 80 B/lane and lost 1.4 %)
+                      // C2/C3 fit 95 VGPRs at 5 waves without spill (C2 2048 spp 178.0 -> 171.6 ms against
+                      // the old 3-wave budget); 6 waves (80 VGPRs, 64 B/lane of spilled loop invariants)
+                      // gain another 2-2.6 % (C2 171.5 -> 167.9, C3 179.5 -> 174.9 ms); 7 waves (72 VGPRs,
+                      // 96 B/lane) lose 10 %
 #endif
 #ifndef PTMI_WAVES_MATERIALS
 #define PTMI_WAVES_MATERIALS 3  // ... with reflective / refractive materials (at 5 they spill 96-112 B/lane)
