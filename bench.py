@@ -23,11 +23,13 @@ traffic is ~0.02 B/sample): achieved = algorithmic FP64 flops per launch (frozen
 model, profiles/alg_counts.json, ptmi/flops.py) / the kernel's average launch
 time, measured with HIP events recorded on the launch stream around every launch
 in the timed region; peak = MI355X FP64 vector peak (78.6 TFLOP/s).  C4/C5 (BVH
-scenes) report the memory-hierarchy roofline of SURVEY.md 8d: bytes per sample of
-the traversal the kernel runs (tools/traversal_bytes.py) over the 8 TB/s HBM
-peak, with the reference visit rules' bytes and the FP64 figure beside it.
-`traffic` is null: HBM bytes come from rocprofv3 PMC passes, which cannot run
-inside this process (profiles/<round>/ holds them).
+scenes) report the memory hierarchy of SURVEY.md 8d level by level: the bytes per
+sample of the traversal the kernel runs (tools/traversal_bytes.py) are L2-served,
+so they are priced against the L2 peak (34.5 TB/s), with the PMC-measured L2
+requests and HBM bytes beside them; the bound is VALU issue / load latency (idle
+lanes in the walk phases), which is what the counters show.  `traffic` = HBM bytes
+per launch from rocprofv3 PMC passes of this build (they cannot run inside this
+process; profiles/pmc_measured.json freezes them from profiles/<round>/).
 cpu_baseline: the oracle's C restatement of the reference kernel (OpenMP) timed on
 the host cores on a bounded sample of the same frame spread over its sample
 indices, plus the whole C1 frame (rank 0, N=1 only).
@@ -56,6 +58,10 @@ CONFIGS = {
 }
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (/opt/skills/guides/MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak
+L2_PEAK_GBS = 34500.0    # MI355X aggregate L2 bandwidth, 8 XCDs x 4 MiB (MI355X_MICROARCH.md "L2 (per XCD)")
+# rocprofv3 PMC measurements of the current build (HBM bytes and L2 requests per trace_kernel
+# launch, per workload), frozen by tools/pmc_freeze.py from the profiles/<round>/ passes.
+PMC_FROZEN = os.path.join(ROOT, "profiles", "pmc_measured.json")
 
 
 def _free_port():
@@ -227,6 +233,19 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
     torch.cuda.set_device(device)
+    # Which GPU each rank landed on (a scaling run must show N distinct devices).
+    props = torch.cuda.get_device_properties(device)
+    me = {"rank": rank, "local_rank": local, "device": device, "name": props.name,
+          "arch": getattr(props, "gcnArchName", None), "uuid": str(getattr(props, "uuid", "")),
+          "pci": "%s:%s:%s" % (getattr(props, "pci_domain_id", "?"), getattr(props, "pci_bus_id", "?"),
+                               getattr(props, "pci_device_id", "?")),
+          "visible_devices": ndev}
+    ranks_info = [me]
+    if world > 1:
+        ranks_info = [None] * world
+        dist.all_gather_object(ranks_info, me)
+    comm = {"backend": dist.get_backend() if world > 1 else "none", "world_size": world,
+            "distinct_devices": len({r["uuid"] or r["pci"] for r in ranks_info}), "ranks": ranks_info}
 
     def run_config(cfg, steps, warmup, samples=0, chunks=0, save_image=""):
         """Render `steps` timed frames of config `cfg` on this rank's share (after
@@ -302,6 +321,7 @@ def main():
             res = {"value": W * H * S * steps / el / 1e6, "ms_per_step": el / steps * 1e3, "image_ok": ok,
                    "avg_kernel_ms": avg_ms, "launches": klaunch, "per_rank": per_rank,
                    "rate": my_samples_per_launch / (avg_ms * 1e-3), "alg_key": alg_key, "split": split,
+                   "samples_per_launch": my_samples_per_launch, "frame_samples": W * H * S,
                    "config": {"workload": desc, "scene": scene_name, "width": W, "height": H, "spp": S,
                               "aperture": aper, "focal_length": focal, "split": split, "parallelism": par}}
         scene.close()
@@ -315,7 +335,13 @@ def main():
                 ac = json.load(f)["workloads"][res["alg_key"]]
         except (OSError, KeyError) as e:
             return {"error": "alg counts unavailable: %s" % e}
+        try:
+            with open(PMC_FROZEN) as f:
+                pmc = json.load(f)["workloads"].get(res["alg_key"])
+        except (OSError, KeyError, ValueError):
+            pmc = None
         rate = res["rate"]  # samples/s of the kernel, rank 0
+        kms = res["avg_kernel_ms"]
         f64 = ac["fp64_flops_per_sample"]
         achieved = f64 * rate / 1e12
         fp64 = {"bound": "valu_fp64",
@@ -323,27 +349,55 @@ def main():
                 "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "fp64_flops_per_sample": round(f64, 1),
                 "flops_basis": "reference-rule algorithmic count (oracle -DPTO_COUNT), not executed"}
+        # HBM bytes per launch measured by rocprofv3 PMC passes of this build (FETCH_SIZE x2 +
+        # WRITE_SIZE, gfx950-corrected), scaled to this launch's share of the frame.
+        share = res["samples_per_launch"] / float(res["frame_samples"])
+        traffic = None
+        hbm = None
+        if pmc and pmc.get("hbm_bytes_per_launch"):
+            traffic = pmc["hbm_bytes_per_launch"] * share
+            gbs = traffic / (kms * 1e-3) / 1e9
+            hbm = {"achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(gbs / HBM_PEAK_GBS, 6), "bytes_per_launch": round(traffic),
+                   "source": pmc.get("source")}
         tv = ac.get("traversal")
         if tv is None:  # C2 / C3: FP64-VALU bound
             roof = dict(fp64)
-        else:  # C4 / C5: memory hierarchy, bytes of the traversal actually run
-            gbs = tv["bytes_per_sample"] * rate / 1e9
+            if hbm:
+                roof["hbm"] = hbm
+        else:
+            # C4 / C5 (SURVEY.md 8d memory hierarchy): the traversal's node / triangle bytes are
+            # served by L2 (working set ~1-2 MB per XCD), so its bandwidth level is L2; HBM beside
+            # it.  Neither binds: the counters show VALU issue with idle lanes and dependent
+            # node-load latency (profiles/<round>/SUMMARY.md), hence the bound.
+            l2_gbs = tv["bytes_per_sample"] * rate / 1e9
             ref_gbs = ac["bytes_per_sample"] * rate / 1e9
-            roof = {"bound": "hbm",
-                    "bound_detail": "memory hierarchy (SURVEY.md 8d): BVH node and triangle fetches; the "
-                                    "working set (~1-2 MB) is L2-resident, so the walk is load-latency bound",
-                    "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(gbs / HBM_PEAK_GBS, 4),
-                    "bytes_per_sample": round(tv["bytes_per_sample"], 1), "bytes_basis": tv["basis"],
+            l2 = {"achieved": round(l2_gbs, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(l2_gbs / L2_PEAK_GBS, 4), "bytes_per_sample": round(tv["bytes_per_sample"], 1),
+                  "bytes_basis": tv["basis"]}
+            if pmc and pmc.get("l2_read_bytes_per_launch"):
+                mb = pmc["l2_read_bytes_per_launch"] * share
+                l2["measured"] = {"bytes_per_launch": round(mb), "GBs": round(mb / (kms * 1e-3) / 1e9, 1),
+                                  "frac": round(mb / (kms * 1e-3) / 1e9 / L2_PEAK_GBS, 4),
+                                  "l2_hit_rate": pmc.get("l2_hit_rate"), "source": pmc.get("source")}
+            roof = {"bound": "valu_issue_latency",
+                    "bound_detail": "VALU issue with idle lanes in the BVH walk phases and the latency of "
+                                    "their dependent node loads; the L2 and HBM levels below are far from "
+                                    "their peaks (the traversal's working set is L2-resident)",
+                    "achieved": l2["achieved"], "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": l2["frac"],
+                    "level": "l2", "l2": l2, "hbm": hbm,
                     "reference_rule": {"bytes_per_sample": round(ac["bytes_per_sample"], 1),
                                        "equivalent_GBs": round(ref_gbs, 1),
                                        "basis": "the reference's visit rules (tracer.cl:617-719: every "
                                                 "triangle of every node whose box the line passes): the "
                                                 "bytes its traversal would fetch at this sample rate"},
                     "fp64_reference_equivalent": fp64}
-        roof.update({"traffic": None,
-                     "traffic_note": "HBM bytes per launch from rocprofv3 PMC passes (profiles/<round>/)",
-                     "kernel": "trace_kernel (rank 0)", "kernel_ms_avg": round(res["avg_kernel_ms"], 3),
+            if pmc and pmc.get("valu"):
+                roof["valu"] = pmc["valu"]
+        roof.update({"traffic": None if traffic is None else round(traffic),
+                     "traffic_note": "HBM bytes per launch, rocprofv3 PMC passes of this build "
+                                     "(profiles/pmc_measured.json <- profiles/<round>/)",
+                     "kernel": "trace_kernel (rank 0)", "kernel_ms_avg": round(kms, 3),
                      "launches": res["launches"]})
         return roof
 
@@ -355,13 +409,14 @@ def main():
     extras = {}
     extra = args.extra
     if extra == "auto":
-        extra = "c3,c5" if args.config == "c2" and not args.samples and not args.chunks else "none"
+        extra = "c3,c4,c5" if args.config == "c2" and not args.samples and not args.chunks else "none"
     for cfg in [c for c in extra.split(",") if c and c != "none" and c != args.config]:
         r, _ = run_config(cfg, args.extra_steps, 1)
         if rank == 0:
+            rf = roofline(r)
             ex = {"value": round(r["value"], 2), "unit": "Msamples/s", "ms_per_step": round(r["ms_per_step"], 3),
                   "steps": args.extra_steps, "warmup": 1, "image_ok": r["image_ok"], "config": r["config"],
-                  "roofline_frac": roofline(r).get("frac")}
+                  "roofline_frac": rf.get("frac"), "roofline": rf}
             if world > 1:
                 ex["per_rank_kernel_ms"] = [round(float(x), 3) for x in r["per_rank"][:, 1]]
                 ex["reduce_ms"] = round(float(r["per_rank"][0, 2]), 3)
@@ -398,6 +453,7 @@ def main():
             "config": res["config"],
             "image_ok": ok, "roofline": roof, "cpu_baseline": cpu, "ptmi_trace_call": inclusive,
         }
+        line["comm"] = comm
         if world > 1:
             line["per_rank"] = {"kernel_ms": [round(float(x), 3) for x in per_rank[:, 1]],
                                 "wall_s": [round(float(x), 4) for x in per_rank[:, 0]],

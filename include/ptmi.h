@@ -93,9 +93,12 @@ int ptmi_trace(const void* objects, uint32_t n_obj, const void* triangles, uint3
  * The host converts the scene and builds its traversal index once; each device
  * uploads it.  The partial frames are combined on the device side: peer copies
  * over xGMI into a gather buffer on devices[0], summed there in device order
- * (deterministic; the tile split is exact, the sample split differs from one
- * device only by FP64 summation order) and normalised as ptmi_finalize, then read
- * back once.  Same record / seed / error contract as ptmi_trace.  (The
+ * (deterministic) and normalised as ptmi_finalize, then read back once.  The
+ * result equals ptmi_trace's up to FP64 summation order: each device plans its own
+ * work items (ptmi_scene_render, chunks = 0), and where that plan splits a tile's
+ * samples into chunks differently from the one-device plan, the tile's per-pixel
+ * sums are added in a different grouping (bit-identical when every tile is one
+ * whole item on both sides, e.g. short sample ranges).  Same record / seed / error contract as ptmi_trace.  (The
  * torch.distributed driver, bench.py, does the same with one process per GPU and
  * an RCCL reduce.)
  */
@@ -111,6 +114,8 @@ typedef struct ptmi_multi_timing {
     double combine_ms;  /* from then: xGMI peer copies into the first device + the ordered sum */
     double readback_ms; /* the RGBA frame to host memory */
     double total_ms;    /* the whole call, releasing the device buffers included */
+    int32_t peer_direct; /* shards on other devices with direct peer (xGMI) access to devices[0] */
+    int32_t peer_staged; /* shards on other devices whose copy the runtime stages (peer access refused) */
 } ptmi_multi_timing;
 
 /* ptmi_trace_multi, also reporting its phases in *timing (may be NULL). */
@@ -119,6 +124,14 @@ int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const void* tria
                            uint32_t samples, const void* camera, const double* seeds, uint64_t seed_stream,
                            const ptmi_textures* textures, double* out_rgba, ptmi_multi_timing* timing, char* err,
                            size_t err_len);
+
+/* The combine step of ptmi_trace_multi, for callers that gather their own partial
+ * frames: parts_dev holds n_parts frames of n_pixels * 4 doubles (RGB sums, A = the
+ * sample count) back to back on one device; out_dev[4i + c] = (sum over parts, in part
+ * order, of part[4i + c]) * (1.0 / samples) for RGB and 1.0 for A (tracer.cl:1184-1187).
+ * out_dev may alias parts_dev (slot 0).  Asynchronous on hip_stream. */
+int ptmi_combine_frames(const double* parts_dev, uint32_t n_parts, uint32_t n_pixels, double* out_dev,
+                        uint32_t samples, void* hip_stream, char* err, size_t err_len);
 
 /* First sample index of device g of n in ptmi_trace_multi's cost-balanced sample
  * split (g = n -> samples); the same table as bench.py's ranks (ptmi/dist.py). */

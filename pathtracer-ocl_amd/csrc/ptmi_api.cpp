@@ -782,6 +782,7 @@ extern "C" int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const
     HIP_TRY(hipSetDevice(root));
     HIP_TRY(hipMalloc((void**)&gather, frame_bytes * n_devices));
     std::vector<int> rcs(n_devices, PTMI_OK);
+    std::vector<int> peer(n_devices, -1);  // per shard: 1 direct peer access, 0 staged copy, -1 root itself
     std::vector<std::string> msgs(n_devices);
     std::vector<clk::time_point> t_rendered(n_devices, t_prep);
     // Per-device resources, released after the combine and read-back (hipFree
@@ -799,11 +800,16 @@ extern "C" int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const
         hipStream_t& st = streams[d];
         drc = upload_scene(hs, dev, textures, &s, e, sizeof(e));
         if (!drc && dev != root) {  // direct xGMI access to the gather buffer where the link allows it
+            // hipMemcpyPeerAsync works without peer access (the runtime stages the copy), so a
+            // refusal is not an error: it is reported (timing->peer_direct) and its sticky error
+            // state is cleared, so it cannot surface later through launch_trace's hipGetLastError.
             int can = 0;
+            peer[d] = 0;
             if (hipDeviceCanAccessPeer(&can, dev, root) == hipSuccess && can) {
                 const hipError_t pe = hipDeviceEnablePeerAccess(root, 0);
-                if (pe == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+                if (pe == hipSuccess || pe == hipErrorPeerAccessAlreadyEnabled) peer[d] = 1;
             }
+            (void)hipGetLastError();
         }
         if (!drc && (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
                      hipMalloc((void**)&d_seeds, npix * sizeof(double)) != hipSuccess ||
@@ -857,9 +863,14 @@ extern "C" int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const
             return rcs[d];
         }
     const clk::time_point t_all_rendered = *std::max_element(t_rendered.begin(), t_rendered.end());
-    HIP_TRY(hipSetDevice(root));
+    hipError_t he = hipSetDevice(root);
+    if (he != hipSuccess) {
+        release();
+        set_err(err, err_len, "hipSetDevice(%d) before the combine: %s", root, hipGetErrorString(he));
+        return PTMI_ERR_HIP;
+    }
     double* frame = gather;  // slot 0 is overwritten in place by the ordered sum
-    hipError_t he = launch_combine(gather, n_devices, npix, frame, samples, nullptr);
+    he = launch_combine(gather, n_devices, npix, frame, samples, nullptr);
     if (he == hipSuccess) he = hipDeviceSynchronize();
     const clk::time_point t_combined = clk::now();
     if (he == hipSuccess) he = hipMemcpy(out_rgba, frame, frame_bytes, hipMemcpyDeviceToHost);
@@ -876,7 +887,21 @@ extern "C" int ptmi_trace_multi_timed(const void* objects, uint32_t n_obj, const
         timing->combine_ms = ms_since(t_all_rendered, t_combined);
         timing->readback_ms = ms_since(t_combined, t_end);
         timing->total_ms = ms_since(t_start, t_done);
+        timing->peer_direct = (int32_t)std::count(peer.begin(), peer.end(), 1);
+        timing->peer_staged = (int32_t)std::count(peer.begin(), peer.end(), 0);
     }
+    return PTMI_OK;
+}
+
+// The device-side combine of ptmi_trace_multi, for callers that gather their own partial
+// frames (one per GPU) into one device buffer: slots summed in slot order, x 1/S, alpha 1.
+extern "C" int ptmi_combine_frames(const double* parts_dev, uint32_t n_parts, uint32_t n_pixels, double* out_dev,
+                                   uint32_t samples, void* hip_stream, char* err, size_t err_len) {
+    if (!parts_dev || !out_dev || n_parts == 0 || samples == 0) {
+        set_err(err, err_len, "bad combine arguments");
+        return PTMI_ERR_ARG;
+    }
+    HIP_TRY(launch_combine(parts_dev, n_parts, n_pixels, out_dev, samples, (hipStream_t)hip_stream));
     return PTMI_OK;
 }
 

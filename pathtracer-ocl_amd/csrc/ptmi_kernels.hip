@@ -74,8 +74,6 @@ static constexpr unsigned kMaxEffectiveBounces = 4;  // tracer.cl:2
 static constexpr unsigned kMaxBounces = 10;          // tracer.cl:3
 static constexpr double kEps = 0.0001;               // tracer.cl:4
 static constexpr double kPi = (double)3.14159265359f;  // tracer.cl:1 (a float literal)
-// Camera-ray batch refill policy (trace_kernel): refill when this many lanes
-// have an empty buffer, or this many lanes are idle waiting for a ray.
 // Camera-ray refill of a wave (trace_kernel): when kRefillNeed lanes have an empty
 // buffer (64: all of them), or kRefillStarve lanes sit idle without a path.  Full
 // batches amortise the camera block; measured on C2 (512 spp): 24/6 61.9 ms,
@@ -89,32 +87,11 @@ static constexpr double kPi = (double)3.14159265359f;  // tracer.cl:1 (a float l
 #ifndef PTMI_REFILL_STARVE_GROUPS
 #define PTMI_REFILL_STARVE_GROUPS 12
 #endif
-#ifndef PTMI_CAM_DEPTH
-#define PTMI_CAM_DEPTH 1  // camera rays buffered per lane (2 and 3 measured no faster on C2)
-#endif
-#ifndef PTMI_CAM_DEPTH_GROUPS
-#define PTMI_CAM_DEPTH_GROUPS 1
-#endif
 static constexpr int kRefillNeed = PTMI_REFILL_NEED;
 #ifndef PTMI_WALK_BATCH
 #define PTMI_WALK_BATCH 24
 #endif
 static constexpr int kWalkBatch = PTMI_WALK_BATCH;  // parked lanes that trigger a wave's BVH walk phase
-#ifndef PTMI_ACC_LDS
-#define PTMI_ACC_LDS 1  // group scenes: per-pixel colour sums in LDS instead of registers
-#endif
-#ifndef PTMI_SINCOS_KMEM
-#define PTMI_SINCOS_KMEM 2  // sincos constants from a __constant__ table (ptmi_fp64core.h): 1 group scenes, 2 all
-#endif
-#ifndef PTMI_HP_LDS
-#define PTMI_HP_LDS 1  // group scenes: a parked lane's primitive best (t, pk) in LDS
-#endif
-#ifndef PTMI_SPHERE_RCP
-#define PTMI_SPHERE_RCP 1  // both sphere roots from one reciprocal (sphere_roots)
-#endif
-#ifndef PTMI_SPHERE_DEFER
-#define PTMI_SPHERE_DEFER 1  // sphere roots evaluated once per lane after the loop (find_closest_prims)
-#endif
 
 struct d4 {
     double x, y, z, w;
@@ -524,19 +501,7 @@ __device__ __forceinline__ void tri_uv(const DevTri& T, d4 o, d4 d, double& u, d
     v = f * dv;
 }
 
-#ifndef PTMI_NV_FOLD
-#define PTMI_NV_FOLD 1
-#endif
-#ifndef PTMI_NV_BRANCHLESS
-#define PTMI_NV_BRANCHLESS 1  // 2048 spp: C4 798 -> 778, C5 1250 -> 1216 ms (no exec-mask branches per child)
-#endif
 static constexpr int kStack = 24;  // per-lane LDS traversal stack (3 pushes x BVH4 depth <= 7, ptmi_bvh.cpp)
-#ifndef PTMI_LDS_NODES
-#define PTMI_LDS_NODES 0  // Node4s staged in LDS per workgroup (the top levels of the index).  0: none --
-                          // every node is a global load (no flat-address select): 2048 spp, C4 808 -> 796,
-                          // C5 1273 -> 1252 ms against 21 (the top 3 levels, 2.3 KB); 1 and 5 in between
-#endif
-static constexpr int kLdsNodes = PTMI_LDS_NODES;
 
 // The reference's gate for one triangle: every reference node on the path from
 // the walked root to the triangle's node passes intersectRayWithBox
@@ -620,14 +585,14 @@ __device__ __forceinline__ void walk_setup(d4 o, d4 rw, float bmax, float rf[3],
 // One Node4 of a walk: its four children tested against the FP32 slabs, the hit
 // ones ordered near-to-far; the far ones are pushed (farthest first) and the
 // nearest is returned in `next` (false: no child hit, pop the stack).
-__device__ __forceinline__ bool node_visit(const DevScene& S, const Node4* lds_nodes, int* __restrict__ stk, int cur,
-                                           int& sp, const float rf[3], const float ofr[3], const float dt[3],
-                                           double ht, int& next) {
+__device__ __forceinline__ bool node_visit(const DevScene& S, int* __restrict__ stk, int cur, int& sp,
+                                           const float rf[3], const float ofr[3], const float dt[3], double ht,
+                                           int& next) {
     PTMI_COUNT(1);
-    // The node's 112 B as seven 16-B loads issued together (one wait), from LDS
-    // for the first kLdsNodes Node4s (the top levels, ptmi_bvh.cpp), else global.
-    const float4* src = cur < kLdsNodes ? reinterpret_cast<const float4*>(lds_nodes) + 7 * cur
-                                        : reinterpret_cast<const float4*>(S.nodes4) + 7 * cur;
+    // The node's 112 B as seven 16-B global loads issued together (one wait).  (Staging
+    // the top levels in LDS made every node fetch a flat load with an aperture select:
+    // C4 796 vs 808, C5 1252 vs 1273 ms per 2048-spp frame without it.)
+    const float4* src = reinterpret_cast<const float4*>(S.nodes4) + 7 * cur;
     float4 q[7];
 #pragma unroll
     for (int u = 0; u < 7; u++) q[u] = src[u];
@@ -646,7 +611,6 @@ __device__ __forceinline__ bool node_visit(const DevScene& S, const Node4* lds_n
         const float ax = fmaf(mnx[i], rf[0], -ofr[0]), bx = fmaf(mxx[i], rf[0], -ofr[0]);
         const float ay = fmaf(mny[i], rf[1], -ofr[1]), by = fmaf(mxy[i], rf[1], -ofr[1]);
         const float az = fmaf(mnz[i], rf[2], -ofr[2]), bz = fmaf(mxz[i], rf[2], -ofr[2]);
-#if PTMI_NV_FOLD
         // Entry clamped at 0 and exit clamped at the pruning limit, so one compare
         // culls a box that is behind the origin (tf < 0), beyond the best hit
         // (tn > lim) or missed (tn > tf).  NaN bounds (a NaN ray) drop out of the
@@ -656,17 +620,6 @@ __device__ __forceinline__ bool node_visit(const DevScene& S, const Node4* lds_n
         const float tn = fmaxf(fmaxf(fmaxf(fminf(ax, bx) - dt[0], fminf(ay, by) - dt[1]), fminf(az, bz) - dt[2]), 0.0f);
         const float tf = fminf(fminf(fminf(fmaxf(ax, bx) + dt[0], fmaxf(ay, by) + dt[1]), fmaxf(az, bz) + dt[2]), lim);
         k[i] = tn > tf ? __builtin_huge_valf() : tn;
-#else
-        const float tn = fmaxf(fmaxf(fminf(ax, bx) - dt[0], fminf(ay, by) - dt[1]), fminf(az, bz) - dt[2]);
-        const float tf = fminf(fminf(fmaxf(ax, bx) + dt[0], fmaxf(ay, by) + dt[1]), fmaxf(az, bz) + dt[2]);
-        // (NaN bounds -- a NaN ray -- fail every test: the child is entered.)
-#if PTMI_NV_BRANCHLESS
-        const bool cull = (tn > tf) | (tn > lim) | (tf < 0.0f) | (c[i] == kEmptyChild);
-#else
-        const bool cull = tn > tf || tn > lim || tf < 0.0f || c[i] == kEmptyChild;
-#endif
-        k[i] = cull ? __builtin_huge_valf() : fmaxf(tn, -__builtin_huge_valf());  // NaN -> -inf
-#endif
     }
     // sort (k, c) ascending: 5 compare-exchanges
 #define PTMI_CX(a, b)                                      \
@@ -680,20 +633,15 @@ __device__ __forceinline__ bool node_visit(const DevScene& S, const Node4* lds_n
     }
     PTMI_CX(0, 1) PTMI_CX(2, 3) PTMI_CX(0, 2) PTMI_CX(1, 3) PTMI_CX(1, 2)
 #undef PTMI_CX
-#if PTMI_NV_BRANCHLESS
-    // unconditional stores above the top, the top advanced by the hit flags (sp <= 21
-    // before a node, so the stores stay inside the 24 entries)
+    // Unconditional stores above the top, the top advanced by the hit flags (sp <= 21
+    // before a node, so the stores stay inside the 24 entries): no exec-mask branches
+    // per child (C4 798 -> 778, C5 1250 -> 1216 ms per 2048-spp frame).
     stk[sp * kStkStride] = c[3];
     sp += k[3] < __builtin_huge_valf() ? 1 : 0;
     stk[sp * kStkStride] = c[2];
     sp += k[2] < __builtin_huge_valf() ? 1 : 0;
     stk[sp * kStkStride] = c[1];
     sp += k[1] < __builtin_huge_valf() ? 1 : 0;
-#else
-    if (k[3] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[3];
-    if (k[2] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[2];
-    if (k[1] < __builtin_huge_valf()) stk[(sp++) * kStkStride] = c[1];
-#endif
     next = c[0];
     return k[0] < __builtin_huge_valf();
 }
@@ -707,9 +655,7 @@ __device__ __forceinline__ void leaf_visit(const DevScene& S, int code, int slot
     PTMI_COUNT(2);
     for (int i = first; i < end; i++) {
         PTMI_COUNT(3);
-#if !(defined(PTMI_EXP) && (PTMI_EXP & 4))
         tri_test<kVerify>(S, S.tris[i], i, o, d, slot, key, h, vchain);
-#endif
     }
 }
 
@@ -718,9 +664,8 @@ __device__ __forceinline__ void leaf_visit(const DevScene& S, int code, int slot
 // not depend on the visiting order or the widened boxes (every triangle that
 // can produce a winning t is reached); ties resolve through better_tri.
 template <bool kVerify>
-__device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes,
-                                           const RootRec& R, int slot, int key, d4 o, d4 d, d4 rw, Hit& h,
-                                           int& vchain) {
+__device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const RootRec& R, int slot,
+                                           int key, d4 o, d4 d, d4 rw, Hit& h, int& vchain) {
     float rf[3], ofr[3], dt[3];  // FP32 slab tests (walk_setup)
     walk_setup(o, rw, R.bmax, rf, ofr, dt);
     int sp = 0;
@@ -738,7 +683,7 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
         PTMI_TSTAMP(t_nd);
         if (cur >= 0) {
             int next;
-            const bool down = node_visit(S, lds_nodes, stk, cur, sp, rf, ofr, dt, h.t, next);
+            const bool down = node_visit(S, stk, cur, sp, rf, ofr, dt, h.t, next);
             PTMI_TADD(29, t_nd);
             if (down) {
                 cur = next;
@@ -786,7 +731,7 @@ __device__ __forceinline__ void sphere_quad(d4 o, d4 d, double& a, double& b, do
 // >= 2^-767 or so small that b is too (then both roots are below EPSILON).
 template <bool A>
 __device__ __forceinline__ void sphere_roots(Hit& h, double a, double b, double disc, int slot, int key) {
-    if (A && PTMI_SPHERE_RCP && !(PTMI_ABLATE & 128)) {
+    if (A && !(PTMI_ABLATE & 128)) {
         // Both roots from one reciprocal of 2a (div_core_r: bit-identical to two div_core
         // calls), then one candidate: t1 if it is one, else t2 -- the reference records
         // both, and t2 >= t1 can only win when t1 <= EPSILON (see below).
@@ -970,10 +915,6 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     double pa = 0.0, pb = 0.0, pd = 0.0;
     int pslot = 0, pkey = 0;
     auto defer = [&](double a, double b, double disc, int slot, int key) {
-        if (!PTMI_SPHERE_DEFER) {
-            sphere_roots<A>(h, a, b, disc, slot, key);
-            return;
-        }
         const bool has = disc > 0.0;
         if (has && pend) sphere_roots<A>(h, a, b, disc, slot, key);
         const bool take = has && !pend;
@@ -1060,9 +1001,6 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
 // triangle on its gate chain (chain_certified / verify_chain).
 template <bool A>
 __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd, const Hit& h) {
-#if defined(PTMI_EXP) && (PTMI_EXP & 2)
-    return false;
-#endif
     for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
         const DevObject& ob = S.objs[j];
         const d4 o = xpt<A>(ob.inv, ob.st, ro);
@@ -1083,11 +1021,8 @@ __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd
 // each improving candidate (exact by construction, slower: the check runs
 // inside the divergent walk loop).
 template <bool A, bool kVerify>
-__device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes, d4 ro,
-                                                 d4 rd, Hit& h, bool& cert) {
-#if defined(PTMI_EXP) && (PTMI_EXP & 1)
-    return;
-#endif
+__device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h,
+                                                 bool& cert) {
     for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
         const DevObject& ob = S.objs[j];
         const d4 o = xpt<A>(ob.inv, ob.st, ro);
@@ -1105,7 +1040,7 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restr
                          R.hull_mx[2], h.t + prune_margin(h.t), tn))
                 continue;
             PTMI_TSTAMP(t_w);
-            walk_index<kVerify>(S, stk, lds_nodes, R, j, ob.key, o, d, r, h, vchain);
+            walk_index<kVerify>(S, stk, R, j, ob.key, o, d, r, h, vchain);
             PTMI_TADD_ACTIVE(18, t_w);  // (stats: cycles in walk loops)
         }
         // Tentative walks: certify the gate chain of a winner from this object while
@@ -1122,12 +1057,10 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restr
 // tests/adversarial.py) are this ray's walks redone with eager checks.  All
 // lanes verify together after the loop instead of one by one inside it.
 template <bool A>
-__device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__ stk, const Node4* lds_nodes, d4 ro, d4 rd,
-                                            Hit& h) {
+__device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
     const Hit h0 = h;
     bool cert = false;
-    group_walks_impl<A, false>(S, stk, lds_nodes, ro, rd, h, cert);
-#if !(defined(PTMI_EXP) && (PTMI_EXP & 8))
+    group_walks_impl<A, false>(S, stk, ro, rd, h, cert);
     if (h.tri >= 0) PTMI_COUNT(4);
     if (h.tri >= 0 && !cert) {  // the winner is a triangle (h0 holds primitives only) without certificate
         const DevObject& ob = S.objs[hit_obj(h)];
@@ -1136,10 +1069,9 @@ __device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__
         if (!verify_chain(S, S.tris[h.ti].chain, o, d)) {
             PTMI_COUNT(11);  // (stats build: eager re-walks)
             h = h0;
-            group_walks_impl<A, true>(S, stk, lds_nodes, ro, rd, h, cert);
+            group_walks_impl<A, true>(S, stk, ro, rd, h, cert);
         }
     }
-#endif
     if (h.tri >= 0) {  // the winner's barycentrics (for its interpolated normal)
         const DevObject& ob = S.objs[hit_obj(h)];
         tri_uv(S.tris[h.ti], xpt<A>(ob.inv, ob.st, ro), xdir<A>(ob.inv, ob.st, rd), h.u, h.v);
@@ -1176,7 +1108,7 @@ template <bool A>
 __device__ __forceinline__ d4 reflect(d4 rd, d4 nv) { return sub4(rd, scl4(scl4(nv, 2.0), dotv<A>(rd, nv))); }
 
 // randomVectorInHemisphere (tracer.cl:348-366); x, y, z hold float-valued doubles.
-template <bool A, bool kKMem>
+template <bool A>
 __device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float fz) {
     double rand1 = 2.0 * kPi * (double)noise3d(fx, fy, fz);
     double rand2 = (double)noise3d(fy, fz, fx);
@@ -1195,7 +1127,7 @@ __device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float
         cr = 1.0 - rand1 * 0.1;
         sr = rand1 * 0.15;
     } else if constexpr (A) {
-        sincos_core<kKMem>(rand1, &sr, &cr);  // rand1 in [0, 2 pi): ocml's sincos without its range steps
+        sincos_core<true>(rand1, &sr, &cr);  // rand1 in [0, 2 pi): ocml's sincos without its range steps
     } else {
         sincos(rand1, &sr, &cr);  // ocml sincos == (sin, cos) bit-for-bit: one shared reduction
     }
@@ -1497,8 +1429,7 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
             reflecting = true;
         }
     } else {
-        P.rd = random_hemisphere<A, PTMI_SINCOS_KMEM == 2 || ((FL & F_GROUPS) != 0 && PTMI_SINCOS_KMEM == 1)>(nv, fgi, (float)b,
-                                                                                              (float)n);
+        P.rd = random_hemisphere<A>(nv, fgi, (float)b, (float)n);
         cosine = dotv<A>(P.rd, nv);
     }
     P.ro = over;
@@ -1548,8 +1479,9 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
     return ob.emission[0] > 0.0 || P.b >= kMaxBounces || P.effective >= kMaxEffectiveBounces;
 }
 
-// grid: x = 4 tiles per block (one 8x8 tile per wave), y = sample chunk.
-// Writes the chunk's RGB sums (A = #samples) to out[(chunk*npix + pixel)*4].
+// One wave per workgroup; workgroup b runs work item b of the WorkPlan: an 8x8 tile
+// over the whole sample range (sums -> the frame) or a sample chunk of a tail tile
+// (sums -> its slot of the partial buffer).  RGB sums, A = #samples.
 template <int FL>
 #ifndef PTMI_WAVES
 #define PTMI_WAVES 6  // waves/SIMD the register allocation targets (scenes without groups or materials).
@@ -1570,16 +1502,6 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
                                                          : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, WorkPlan WP,
                                                     const double* __restrict__ seeds, const double* __restrict__ sunf,
                                                     double* __restrict__ sums, double* __restrict__ part) {
-    // Top levels of the traversal index in LDS (group scenes), staged by the whole
-    // workgroup before any wave can leave.  Entries past n_nodes4 are never read.
-    __shared__ float4 node_lds4[(FL & F_GROUPS) ? (kLdsNodes > 0 ? kLdsNodes : 1) * 7 : 1];
-    const Node4* node_lds = reinterpret_cast<const Node4*>(node_lds4);
-    if constexpr ((FL & F_GROUPS) != 0 && kLdsNodes > 0) {
-        const int nl = min(kLdsNodes, S.n_nodes4) * 7;
-        const float4* src = reinterpret_cast<const float4*>(S.nodes4);
-        for (int k = threadIdx.x; k < nl; k += kBlock) node_lds4[k] = src[k];
-        __syncthreads();
-    }
 #if PTMI_STATS
     if ((threadIdx.x & 63) < 32) ptmi_wstat[threadIdx.x >> 6][threadIdx.x & 63] = 0;
 #endif
@@ -1624,7 +1546,7 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
     double cr = 0.0, cg = 0.0, cb = 0.0;  // colors (tracer.cl:1179)
     // Group scenes may keep the sums in LDS (one slot per lane, the same additions in the
     // same order): they change once per path, and the walk phases need the registers.
-    constexpr bool kAccLds = (FL & F_GROUPS) != 0 && PTMI_ACC_LDS;
+    constexpr bool kAccLds = (FL & F_GROUPS) != 0;
     __shared__ double acc_lds[kAccLds ? 3 * kBlock : 1];
     if constexpr (kAccLds) {
         acc_lds[0 * kBlock + threadIdx.x] = 0.0;
@@ -1641,7 +1563,7 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
     // scenes keep no w lanes.  Group scenes stay one deep (their LDS holds the
     // traversal stacks and nodes).
     constexpr int kCamComp = A ? 6 : 8;
-    constexpr int kCamDepth = (FL & F_GROUPS) ? PTMI_CAM_DEPTH_GROUPS : PTMI_CAM_DEPTH;
+    constexpr int kCamDepth = 1;  // (2- and 3-deep rings measured no faster on C2, +1.4 % on the group scenes)
     constexpr int kB = kBlock;  // LDS stride of the per-lane camera slots
     __shared__ double cam_lds[kCamDepth * kCamComp * kB];
     const int tid = threadIdx.x;
@@ -1654,10 +1576,10 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
     int nb = 0, hb = 0;   // buffered camera rays (samples n_gen - nb ...) and the head slot
     bool active = false, pending = false;
     PathState P;
-    Hit hp;
-    constexpr bool kHpLds = (FL & F_GROUPS) != 0 && PTMI_HP_LDS;
-    __shared__ double hp_t_lds[kHpLds ? kBlock : 1];
-    __shared__ int hp_pk_lds[kHpLds ? kBlock : 1];
+    // A parked lane's primitive best (t, pk) waits in LDS (group scenes): registers are
+    // what the walk phases need.
+    __shared__ double hp_t_lds[(FL & F_GROUPS) ? kBlock : 1];
+    __shared__ int hp_pk_lds[(FL & F_GROUPS) ? kBlock : 1];
     PTMI_TSTAMP(t_loop);
     for (;;) {
         if (!__any(active || nb > 0 || n_gen < c_end)) break;
@@ -1725,12 +1647,8 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
                 h = find_closest_prims<FL>(S, P.ro, P.rd);
                 if ((FL & F_GROUPS) && group_needs_walk<A>(S, P.ro, P.rd, h)) {
                     pending = true;
-                    if constexpr (kHpLds) {  // find_closest_prims: tri, ti, u, v are constants
-                        hp_t_lds[threadIdx.x] = h.t;
-                        hp_pk_lds[threadIdx.x] = h.pk;
-                    } else {
-                        hp = h;
-                    }
+                    hp_t_lds[threadIdx.x] = h.t;  // find_closest_prims: tri, ti, u, v are constants
+                    hp_pk_lds[threadIdx.x] = h.pk;
                 } else {
                     ready = true;
                 }
@@ -1744,12 +1662,8 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
                 PTMI_WADD(8, 1ull);
                 PTMI_WADD(9, (unsigned long long)n_pend);
                 if (pending) {
-                    if constexpr (kHpLds) {
-                        h = Hit{hp_t_lds[threadIdx.x], hp_pk_lds[threadIdx.x], -1, -1, 0.0, 0.0};
-                    } else {
-                        h = hp;
-                    }
-                    group_walks<A>(S, stk, node_lds, P.ro, P.rd, h);
+                    h = Hit{hp_t_lds[threadIdx.x], hp_pk_lds[threadIdx.x], -1, -1, 0.0, 0.0};
+                    group_walks<A>(S, stk, P.ro, P.rd, h);
                     pending = false;
                     ready = true;
                 }

@@ -28,12 +28,13 @@ PTMI_OK, PTMI_ERR_ARG, PTMI_ERR_DEVICE, PTMI_ERR_HIP, PTMI_ERR_UNSUPPORTED, PTMI
 EXPORTS = ("ptmi_trace", "ptmi_device_count", "ptmi_device_name", "ptmi_scene_create", "ptmi_scene_destroy",
            "ptmi_scene_size", "ptmi_scene_render", "ptmi_finalize", "ptmi_fill_seeds", "ptmi_build_info",
            "ptmi_scene_set_timing", "ptmi_scene_kernel_time", "ptmi_trace_multi", "ptmi_scene_create_textured",
-           "ptmi_trace_multi_timed", "ptmi_sample_split_point")
+           "ptmi_trace_multi_timed", "ptmi_sample_split_point", "ptmi_combine_frames")
 
 
 class MultiTiming(ctypes.Structure):
     """ptmi_multi_timing (include/ptmi.h): wall-clock phases of ptmi_trace_multi, ms."""
-    _fields_ = [(n, ctypes.c_double) for n in ("prepare_ms", "render_ms", "combine_ms", "readback_ms", "total_ms")]
+    _fields_ = [(n, ctypes.c_double) for n in ("prepare_ms", "render_ms", "combine_ms", "readback_ms", "total_ms")] + \
+        [("peer_direct", ctypes.c_int32), ("peer_staged", ctypes.c_int32)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -68,6 +69,8 @@ def load_library(path=None):
     lib.ptmi_trace_multi_timed.restype = i32
     lib.ptmi_trace_multi_timed.argtypes = [vp, u32, vp, u32, vp, u32, vp, u32, i32, u32, vp, vp, ctypes.c_uint64, vp,
                                            vp, ctypes.POINTER(MultiTiming), cp, sz]
+    lib.ptmi_combine_frames.restype = i32
+    lib.ptmi_combine_frames.argtypes = [vp, u32, u32, vp, u32, vp, cp, sz]
     lib.ptmi_sample_split_point.restype = u32
     lib.ptmi_sample_split_point.argtypes = [i32, i32, u32]
     lib.ptmi_device_count.restype = i32
@@ -183,6 +186,15 @@ def TraceMulti(objects, triangles, groups, devices, split, samples, camera, text
                                     out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(timing), err, len(err))
     _check(rc, err)
     return out, timing.as_dict()
+
+
+def combine_frames(parts_ptr, n_parts, n_pixels, out_ptr, samples, stream=0):
+    """ptmi_combine_frames: n_parts partial frames (device memory, back to back) summed
+    in part order and normalised into out_ptr (may equal parts_ptr)."""
+    err = ctypes.create_string_buffer(256)
+    _check(load_library().ptmi_combine_frames(ctypes.c_void_p(parts_ptr), int(n_parts), int(n_pixels),
+                                              ctypes.c_void_p(out_ptr), int(samples), ctypes.c_void_p(stream),
+                                              err, len(err)), err)
 
 
 def sample_split_point(g, n, samples):

@@ -303,3 +303,31 @@ def test_trace_multi_matches_single_device(scene, w, h, spp, split, ndev):
     else:
         assert np.abs(out - single).max() < 1e-12
     assert all(timing[k] >= 0 for k in timing) and timing["total_ms"] >= timing["render_ms"]
+
+
+def test_combine_frames_sums_distinct_slots_in_slot_order():
+    """ptmi_combine_frames (the combine of ptmi_trace_multi) over 8 slots with distinct
+    contents whose sum depends on the order of addition: equal bit for bit to the sums
+    taken left to right in slot order, x (1.0 / S), alpha 1 (tracer.cl:1184-1187)."""
+    import torch
+    npix, nparts, S = 4096 + 37, 8, 1000
+    rng = np.random.default_rng(5)
+    # magnitudes spread over many binades, so FP64 addition is far from associative here
+    parts = rng.standard_normal((nparts, npix, 4)) * np.exp2(rng.integers(-30, 30, (nparts, npix, 4)))
+    parts[:, :, 3] = rng.integers(0, 300, (nparts, npix))
+    want = parts[0, :, :3].copy()
+    for k in range(1, nparts):
+        want = want + parts[k, :, :3]
+    want = want * (1.0 / S)
+    shuffled = parts[::-1].sum(axis=0)[:, :3] * (1.0 / S)
+    assert not np.array_equal(want, shuffled)  # the test can see an ordering error
+    d = torch.tensor(parts.reshape(-1), dtype=torch.float64, device="cuda")
+    out = torch.empty(npix * 4, dtype=torch.float64, device="cuda")
+    api.combine_frames(d.data_ptr(), nparts, npix, out.data_ptr(), S)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(npix, 4)
+    assert np.array_equal(got[:, :3], want)
+    assert np.all(got[:, 3] == 1.0)
+    api.combine_frames(d.data_ptr(), nparts, npix, d.data_ptr(), S)  # in place into slot 0
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy().reshape(nparts, npix, 4)[0], got)

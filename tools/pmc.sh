@@ -18,5 +18,5 @@ for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || echo "pass $i failed ($P)" >> $OUT/failed.txt
 done
-python3 tools/pmc_summary.py $OUT > $OUT/summary.txt 2>&1 || true
+python3 tools/pmc_summary.py $OUT --valu-json $OUT/valu.json > $OUT/summary.txt 2>&1 || true
 cat $OUT/summary.txt

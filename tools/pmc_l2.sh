@@ -11,5 +11,5 @@ for P in "TCC_HIT_sum TCC_MISS_sum" "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_R
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1
 done
-python3 tools/pmc_summary.py $OUT > $OUT/summary.txt 2>&1 || true
+python3 tools/pmc_summary.py $OUT --l2-json $OUT/l2.json > $OUT/summary.txt 2>&1 || true
 cat $OUT/summary.txt
