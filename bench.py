@@ -247,7 +247,7 @@ def main():
     comm = {"backend": dist.get_backend() if world > 1 else "none", "world_size": world,
             "distinct_devices": len({r["uuid"] or r["pci"] for r in ranks_info}), "ranks": ranks_info}
 
-    def run_config(cfg, steps, warmup, samples=0, chunks=0, save_image=""):
+    def run_config(cfg, steps, warmup, samples=0, chunks=0, save_image="", rng=0):
         """Render `steps` timed frames of config `cfg` on this rank's share (after
         `warmup` untimed ones): barrier + synchronize on both sides, max over ranks.
         Returns (per-config results on rank 0, the scene inputs)."""
@@ -256,6 +256,8 @@ def main():
             S = samples
         objs, tris, grps, cam = scene_inputs(scene_name, W, H, aper, focal)
         scene = api.Scene(device, objs, tris, grps, cam)
+        if rng:
+            scene.set_rng(rng)  # the opt-in statistical mode: never the headline value
         npix = W * H
         seeds_host = layout.seeds_go_float64(npix, 1234)
         seeds = torch.tensor(seeds_host, dtype=torch.float64, device="cuda")
@@ -407,6 +409,19 @@ def main():
     # (C3 / C5 are the reference's 8-GPU configurations; the driver's 1/2/4/8 runs then
     # measure their scaling too).  Secondary: `value` and `ms_per_step` are the headline's.
     extras = {}
+    # The opt-in statistical RNG mode (xoshiro128**, ptmi_scene_set_rng) on the headline
+    # config, reported under its own key: its images are not the reference's, so it is
+    # never `value`.
+    stat_rng = None
+    if args.extra == "auto" and args.config == "c2" and not args.samples and not args.chunks:
+        r, _ = run_config("c2", args.extra_steps, 1, rng=api.RNG_XOSHIRO)
+        if rank == 0:
+            stat_rng = {"value": round(r["value"], 2), "unit": "Msamples/s", "ms_per_step": round(r["ms_per_step"], 3),
+                        "avg_kernel_ms": round(r["avg_kernel_ms"], 3), "steps": args.extra_steps, "warmup": 1,
+                        "image_ok": r["image_ok"],
+                        "what": "C2 with the opt-in statistical RNG (xoshiro128** per path instead of the "
+                                "reference's noise3D): converges to the same image, does not equal it "
+                                "(tests/test_gpu_rng_mode.py); not comparable to `value`"}
     extra = args.extra
     if extra == "auto":
         extra = "c3,c4,c5" if args.config == "c2" and not args.samples and not args.chunks else "none"
@@ -460,6 +475,8 @@ def main():
                                 "reduce_ms": round(float(per_rank[0, 2]), 3), "shared_devices": shared}
         if extras:
             line["extra_configs"] = extras
+        if stat_rng:
+            line["statistical_rng"] = stat_rng
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -189,6 +189,17 @@ int ptmi_finalize(const double* sums_dev, double* out_dev, uint32_t n_pixels, ui
 int ptmi_fill_seeds(double* seeds_dev, uint32_t n, uint64_t seed_stream, void* hip_stream, char* err,
                     size_t err_len);
 
+/* Random numbers of the scene's renders.  PTMI_RNG_NOISE3D (the default) is the
+ * reference's noise3D hash (tracer.cl:314-317, called at :869, 982, 993, 1014, 1038,
+ * 1057), bit for bit: images equal the reference kernel's.  PTMI_RNG_XOSHIRO is an
+ * opt-in STATISTICAL mode: the same uniforms drawn from xoshiro128**, one stream per
+ * (pixel, sample) path seeded from the pixel's seed and the sample index (SplitMix64),
+ * so images are deterministic and independent of the work split, and converge to the
+ * same expectation as the parity mode, but do not equal the reference's.  Affine,
+ * untextured scenes only (else PTMI_ERR_UNSUPPORTED). */
+enum { PTMI_RNG_NOISE3D = 0, PTMI_RNG_XOSHIRO = 1 };
+int ptmi_scene_set_rng(ptmi_scene* s, int mode, char* err, size_t err_len);
+
 /* Kernel timing: with timing enabled, every trace_kernel launch of the scene is
  * bracketed by HIP events recorded on the launch stream; ptmi_scene_kernel_time
  * waits for them, returns the summed kernel milliseconds and launch count since

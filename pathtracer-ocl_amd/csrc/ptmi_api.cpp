@@ -49,6 +49,7 @@ struct ptmi_scene {
     uint32_t tail_tiles = 0;  // chunked tiles at the end of an automatic launch; 0: default (see render)
     uint32_t width = 0, height = 0;
     int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
+    int rng = PTMI_RNG_NOISE3D;  // ptmi_scene_set_rng: PTMI_RNG_XOSHIRO launches the F_XRNG instantiations
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pending (start, stop) pairs
     std::vector<hipEvent_t> spare;
@@ -381,6 +382,22 @@ int prepare_scene(const void* objects, uint32_t n_obj, const void* triangles, ui
     return PTMI_OK;
 }
 
+// Device-wide resident tile waves of the scene's trace_kernel instantiation (its work
+// plan is sized by them, ptmi_scene_render).
+hipError_t resident_waves(ptmi_scene* s) {
+    hipDeviceProp_t p;
+    hipError_t e = hipGetDeviceProperties(&p, s->device);
+    if (e != hipSuccess) return e;
+    const int flags = s->flags | (s->rng == PTMI_RNG_XOSHIRO ? 64 : 0);  // F_XRNG
+    s->resident_waves = p.multiProcessorCount * 16;
+    int blocks_per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, trace_kernel_symbol(flags),
+                                                     trace_block_threads(flags), 0) == hipSuccess &&
+        blocks_per_cu > 0)
+        s->resident_waves = p.multiProcessorCount * blocks_per_cu * trace_tiles_per_block(flags);
+    return hipSuccess;
+}
+
 int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* textures, ptmi_scene** out, char* err,
                  size_t err_len) {
     HIP_TRY(hipSetDevice(device_index));
@@ -454,15 +471,7 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     if (const char* t = getenv("PTMI_TAIL_TILES")) s->tail_tiles = (uint32_t)atoi(t);  // testing: small frames with whole tiles
     s->dev.n_tri = hs.n_tri;
     s->dev.cam = hs.cam;
-    hipDeviceProp_t p;
-    SCENE_TRY(hipGetDeviceProperties(&p, device_index));
-    s->resident_waves = p.multiProcessorCount * 16;  // refined below from the occupancy query
-    int blocks_per_cu = 0;
-    const int block = trace_block_threads(s->flags);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, trace_kernel_symbol(s->flags), block, 0) ==
-            hipSuccess &&
-        blocks_per_cu > 0)
-        s->resident_waves = p.multiProcessorCount * blocks_per_cu * trace_tiles_per_block(s->flags);  // tile waves
+    SCENE_TRY(resident_waves(s));
 #undef SCENE_TRY
     *out = s;
     return PTMI_OK;
@@ -617,12 +626,28 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         s->partial_bytes = need;
     }
     if (ev0) HIP_TRY(hipEventRecord(ev0, st));
-    HIP_TRY(launch_trace(s->dev, s->flags, samples, wp, seeds_dev, s->sunf, sums_dev, s->partial, st));
+    HIP_TRY(launch_trace(s->dev, s->flags | (s->rng == PTMI_RNG_XOSHIRO ? 64 : 0), samples, wp, seeds_dev, s->sunf,
+                         sums_dev, s->partial, st));
     if (ev1) {
         HIP_TRY(hipEventRecord(ev1, st));
         s->events.emplace_back(ev0, ev1);
     }
     HIP_TRY(launch_reduce(s->partial, sums_dev, wp, (int)W, (int)H, st));
+    return PTMI_OK;
+}
+
+int ptmi_scene_set_rng(ptmi_scene* s, int mode, char* err, size_t err_len) {
+    if (!s || (mode != PTMI_RNG_NOISE3D && mode != PTMI_RNG_XOSHIRO)) {
+        set_err(err, err_len, "ptmi_scene_set_rng: bad scene or mode %d", mode);
+        return PTMI_ERR_ARG;
+    }
+    if (mode == PTMI_RNG_XOSHIRO && (s->flags & (16 | 32))) {  // F_PROJ | F_TEX
+        set_err(err, err_len, "the statistical RNG mode exists for affine, untextured scenes only");
+        return PTMI_ERR_UNSUPPORTED;
+    }
+    s->rng = mode;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(resident_waves(s));
     return PTMI_OK;
 }
 

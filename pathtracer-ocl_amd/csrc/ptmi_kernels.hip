@@ -43,7 +43,7 @@ __device__ unsigned long long ptmi_stats[40];
 // Per-wave accumulators (one writer per wave: the first active lane), flushed to
 // ptmi_stats with one atomic per counter when the wave leaves its loop, so clock
 // and per-wave counts do not serialise on global atomics.
-__shared__ unsigned long long ptmi_wstat[4][32];
+__shared__ unsigned long long ptmi_wstat[8][32];
 #define PTMI_FIRST_ACTIVE() ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1)
 #define PTMI_WADD(i, v)                                                \
     do {                                                               \
@@ -88,10 +88,6 @@ static constexpr double kPi = (double)3.14159265359f;  // tracer.cl:1 (a float l
 #define PTMI_REFILL_STARVE_GROUPS 12
 #endif
 static constexpr int kRefillNeed = PTMI_REFILL_NEED;
-#ifndef PTMI_WALK_BATCH
-#define PTMI_WALK_BATCH 24
-#endif
-static constexpr int kWalkBatch = PTMI_WALK_BATCH;  // parked lanes that trigger a wave's BVH walk phase
 
 struct d4 {
     double x, y, z, w;
@@ -262,6 +258,46 @@ __device__ __forceinline__ float noise3d(float x, float y, float z) {
     return fminf(v - floorf(v), 0x1.fffffep-1f);
 }
 
+// ---- Opt-in statistical RNG (F_XRNG, ptmi_scene_set_rng) ---------------------------
+// The reference's noise3D (above) is a hash of (seed, sample, bounce) through a float
+// sin with large-argument reductions -- the parity path keeps it bit for bit.  The
+// statistical mode draws the same uniforms from xoshiro128** (Blackman & Vigna): one
+// stream per path, seeded from the pixel's seed bits and the sample index through
+// SplitMix64, so the image does not depend on which lane, chunk or GPU traces a
+// sample; the camera's two anti-aliasing offsets come from a separate SplitMix64 draw
+// of the same pair.  Uniform floats are the top 24 bits x 2^-24, in [0, 1) like fract.
+struct Xrng {
+    uint32_t s0, s1, s2, s3;
+};
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+__device__ __forceinline__ float xnext(Xrng& r) {
+    const uint32_t res = rotl32(r.s1 * 5u, 7) * 9u;
+    const uint32_t t = r.s1 << 9;
+    r.s2 ^= r.s0;
+    r.s3 ^= r.s1;
+    r.s1 ^= r.s2;
+    r.s0 ^= r.s3;
+    r.s2 ^= t;
+    r.s3 = rotl32(r.s3, 11);
+    return (float)(res >> 8) * 0x1p-24f;
+}
+__device__ __forceinline__ Xrng xseed(uint64_t seed_bits, uint32_t n) {
+    const uint64_t base = seed_bits ^ (0x9E3779B97F4A7C15ull * ((uint64_t)n + 1));
+    const uint64_t a = splitmix64(base + 0x9E3779B97F4A7C15ull), b = splitmix64(base + 0x3C6EF372FE94F82Aull);
+    Xrng r{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+    if ((r.s0 | r.s1 | r.s2 | r.s3) == 0) r.s0 = 1;  // the all-zero state is the one fixed point
+    return r;
+}
+__device__ __forceinline__ void xcamera(uint64_t seed_bits, uint32_t n, float& rx, float& ry) {
+    const uint64_t v = splitmix64(seed_bits + 0xD1B54A32D192ED03ull * ((uint64_t)n + 1));
+    rx = (float)(uint32_t)(v >> 40) * 0x1p-24f;
+    ry = (float)(uint32_t)((v >> 16) & 0xFFFFFFu) * 0x1p-24f;
+}
 // checkAxis (tracer.cl:250-268)
 __device__ __forceinline__ void check_axis(double o, double d, double mn, double mx, double& t0, double& t1) {
     double a0 = mn - o, a1 = mx - o;
@@ -337,20 +373,50 @@ enum : int {
     F_DOF = 8,        // camera aperture != 0
     F_ALL = 15,
     F_PROJ = 16,      // not affine (see dotv): the literal double4 arithmetic, generic path only
-    F_TEX = 32        // textured objects: with F_ALL | F_PROJ, the one textured instantiation
+    F_TEX = 32,       // textured objects: with F_ALL | F_PROJ, the one textured instantiation
+    F_XRNG = 64       // opt-in statistical mode (ptmi_scene_set_rng): xoshiro128** instead of noise3D,
+                      // affine instantiations only; never the parity path
 };
+
+// The camera ray's two anti-aliasing offsets of sample n (tracer.cl:869).
+template <int FL>
+__device__ __forceinline__ void camera_offsets(float fgi, float fgi2, uint64_t seed_bits, uint32_t n, float& rx,
+                                               float& ry) {
+    if constexpr ((FL & F_XRNG) != 0) {
+        xcamera(seed_bits, n, rx, ry);
+    } else {
+        rx = noise3d(fgi, (float)n, fgi2);
+        ry = noise3d(fgi, fgi2, (float)n);
+    }
+}
+
 // Threads per workgroup of trace_kernel: one wave.  A wave that finishes its work
 // item frees its slot (LDS included) at once; with 4-wave groups the slot waited for
 // the slowest of the four (measured, 256 spp: teapot 118.9 -> 116.7 ms, gopher
 // 189.0 -> 177.1 ms, C2 236.0 -> 235.3 ms per 2048 spp).  BVH scenes then stage
 // only the top 3 levels of the traversal index per group (kLdsNodes).
-#ifndef PTMI_BLOCK
-#define PTMI_BLOCK 64
+static constexpr int kBlock = 64;
+// Scenes with BVH groups run workgroups of kTracers tracer waves and kWalkers walker
+// waves sharing a pool of BVH walk requests in LDS (WalkPool); the other scenes one
+// wave per group.
+#ifndef PTMI_TRACERS
+#define PTMI_TRACERS 3
 #endif
-static constexpr int kBlock = PTMI_BLOCK;
-// Per-lane traversal stacks are lane-interleaved across the workgroup: entry k of
-// thread t at [k * kStkStride + t].
-static constexpr int kStkStride = kBlock;
+#ifndef PTMI_WALKERS
+#define PTMI_WALKERS 1
+#endif
+static constexpr int kTracers = PTMI_TRACERS;  // tracer waves per group workgroup
+static constexpr int kWalkers = PTMI_WALKERS;  // walker waves per group workgroup
+static constexpr int kGroupWaves = kTracers + kWalkers;
+static constexpr int kGB = 64 * kGroupWaves;
+static_assert(kTracers >= 1 && kWalkers >= 1 && kGroupWaves <= 8, "tracers and walkers per group");
+template <int FL>
+struct Launch {
+    static constexpr int threads = (FL & 1) ? kGB : kBlock;  // FL & F_GROUPS
+};
+// The walker's per-lane traversal stacks are lane-interleaved: entry k of lane t at
+// [k * kStkStride + t].
+static constexpr int kStkStride = 64;
 
 
 // intersectRayWithBox (tracer.cl:270-280) returning the line's slab interval.
@@ -426,9 +492,8 @@ __device__ __forceinline__ bool ray_box_ref(d4 o, d4 d, d4 r, const double* mn, 
 __device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o, d4 d);
 __device__ __forceinline__ bool chain_certified(const DevScene& S, int chain, d4 o, d4 d, double t);
 
-template <bool kVerify>
 __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, int ti, d4 o, d4 d, int slot, int key,
-                                         Hit& h, int& vchain) {
+                                         Hit& h, int& vchain, bool verify) {
     const double e1x = T.e1[0], e1y = T.e1[1], e1z = T.e1[2];
     const double e2x = T.e2[0], e2y = T.e2[1], e2z = T.e2[2];
     // dirCrossE2 = cross(d, e2)
@@ -464,9 +529,9 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, int
         const int c = T.chain;
         // Eager mode admits the hit only if the reference would have tested this
         // triangle: its gate chain (root -> its node) passes the exact line-box
-        // tests.  The fast mode takes it tentatively; group_walks verifies the
+        // tests.  The fast mode takes it tentatively; walker_loop verifies the
         // final winner.
-        if (kVerify && c != vchain) {
+        if (verify && c != vchain) {
             if (!chain_certified(S, c, o, d, t) && !verify_chain(S, c, o, d)) {
                 PTMI_COUNT(5);  // (stats build: gate rejections)
                 return;
@@ -647,60 +712,15 @@ __device__ __forceinline__ bool node_visit(const DevScene& S, int* __restrict__ 
 }
 
 // The triangles of one leaf (code = first << 3 | count).
-template <bool kVerify>
 __device__ __forceinline__ void leaf_visit(const DevScene& S, int code, int slot, int key, d4 o, d4 d, Hit& h,
-                                           int& vchain) {
+                                           int& vchain, bool verify) {
     PTMI_WADD(31, 1ull);
     const int first = code >> 3, end = first + (code & 7);
     PTMI_COUNT(2);
     for (int i = first; i < end; i++) {
         PTMI_COUNT(3);
-        tri_test<kVerify>(S, S.tris[i], i, o, d, slot, key, h, vchain);
+        tri_test(S, S.tris[i], i, o, d, slot, key, h, vchain, verify);
     }
-}
-
-// Closest-hit walk of one root's 4-wide traversal index (ptmi_bvh.cpp): nearest
-// child first, the others pushed far-to-near.  Which triangles are FOUND does
-// not depend on the visiting order or the widened boxes (every triangle that
-// can produce a winning t is reached); ties resolve through better_tri.
-template <bool kVerify>
-__device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const RootRec& R, int slot,
-                                           int key, d4 o, d4 d, d4 rw, Hit& h, int& vchain) {
-    float rf[3], ofr[3], dt[3];  // FP32 slab tests (walk_setup)
-    walk_setup(o, rw, R.bmax, rf, ofr, dt);
-    int sp = 0;
-    int cur = R.entry;
-    PTMI_COUNT(0);
-#if PTMI_STATS == 1
-    int n_steps = 0, n_leaves = 0;  // (stats: walks that end at the root / without a leaf)
-#endif
-    while (true) {
-#if PTMI_STATS == 1
-        n_steps++;
-        n_leaves += (cur < 0 && cur != kEmptyChild) ? 1 : 0;
-#endif
-        PTMI_COUNT_ACTIVE(19);  // (stats: wave-level walk loop iterations)
-        PTMI_TSTAMP(t_nd);
-        if (cur >= 0) {
-            int next;
-            const bool down = node_visit(S, stk, cur, sp, rf, ofr, dt, h.t, next);
-            PTMI_TADD(29, t_nd);
-            if (down) {
-                cur = next;
-                continue;
-            }
-        } else if (cur != kEmptyChild) {
-            PTMI_TSTAMP(t_lf);
-            leaf_visit<kVerify>(S, -cur - 1, slot, key, o, d, h, vchain);
-            PTMI_TADD(30, t_lf);
-        }
-        if (sp == 0) break;
-        cur = stk[(--sp) * kStkStride];
-    }
-#if PTMI_STATS == 1
-    if (n_leaves == 0) PTMI_COUNT(20);
-    if (n_steps == 1) PTMI_COUNT(21);
-#endif
 }
 
 // Candidate update as selects (no exec-mask branching).  t > EPSILON implies
@@ -993,12 +1013,12 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     return h;
 }
 
-// Groups (tracer.cl:598-720), split in two so a wave can defer the walks
-// (see trace_kernel): group_needs_walk is the cheap part -- the conservative cull
-// of each object's traversal hull against the current best -- and group_walks
-// walks every index that survives, updating h.  The reference's exact box gates
-// (the object's, tracer.cl:609, and its nodes', 617-719) are checked per winning
-// triangle on its gate chain (chain_certified / verify_chain).
+// Groups (tracer.cl:598-720), split in two so the walks can be pooled (WalkPool):
+// group_needs_walk is the cheap part -- the conservative cull of each object's
+// traversal hull against the current best -- and walker_loop walks every index that
+// survives, updating the best.  The reference's exact box gates (the object's,
+// tracer.cl:609, and its nodes', 617-719) are checked per winning triangle on its
+// gate chain (chain_certified / verify_chain).
 template <bool A>
 __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd, const Hit& h) {
     for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
@@ -1015,67 +1035,6 @@ __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd
         }
     }
     return false;
-}
-
-// The walks of every group object for one ray.  kVerify: eager gate checks on
-// each improving candidate (exact by construction, slower: the check runs
-// inside the divergent walk loop).
-template <bool A, bool kVerify>
-__device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h,
-                                                 bool& cert) {
-    for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
-        const DevObject& ob = S.objs[j];
-        const d4 o = xpt<A>(ob.inv, ob.st, ro);
-        const d4 d = xdir<A>(ob.inv, ob.st, rd);
-        const d4 r = mk(rcp_walk(d.x), rcp_walk(d.y), rcp_walk(d.z), 0.0);
-        PTMI_COUNT(7);
-        // The object's own gate (tracer.cl:609) is the first box of every triangle's
-        // gate chain, so it is checked with the rest of the chain (chain_certified /
-        // verify_chain), not here.
-        int vchain = -1;
-        for (int ci = 0; ci < ob.child_count; ci++) {
-            const RootRec& R = S.root_rec[ob.child_base + ci];
-            double tn;
-            if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
-                         R.hull_mx[2], h.t + prune_margin(h.t), tn))
-                continue;
-            PTMI_TSTAMP(t_w);
-            walk_index<kVerify>(S, stk, R, j, ob.key, o, d, r, h, vchain);
-            PTMI_TADD_ACTIVE(18, t_w);  // (stats: cycles in walk loops)
-        }
-        // Tentative walks: certify the gate chain of a winner from this object while
-        // its object-space ray is at hand (a later object that takes over re-certifies).
-        if (!kVerify && h.tri >= 0 && hit_obj(h) == j) cert = chain_certified(S, S.tris[h.ti].chain, o, d, h.t);
-    }
-}
-
-
-// Deferred gate verification.  The walks first take every Moller-Trumbore hit
-// tentatively; their winner is the minimum over a SUPERSET of the reference's
-// candidates, so if it passes its own gate chain it is the reference's winner.
-// Only then (a lane whose winner fails -- seen only with degenerate boxes, see
-// tests/adversarial.py) are this ray's walks redone with eager checks.  All
-// lanes verify together after the loop instead of one by one inside it.
-template <bool A>
-__device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
-    const Hit h0 = h;
-    bool cert = false;
-    group_walks_impl<A, false>(S, stk, ro, rd, h, cert);
-    if (h.tri >= 0) PTMI_COUNT(4);
-    if (h.tri >= 0 && !cert) {  // the winner is a triangle (h0 holds primitives only) without certificate
-        const DevObject& ob = S.objs[hit_obj(h)];
-        const d4 o = xpt<A>(ob.inv, ob.st, ro);
-        const d4 d = xdir<A>(ob.inv, ob.st, rd);
-        if (!verify_chain(S, S.tris[h.ti].chain, o, d)) {
-            PTMI_COUNT(11);  // (stats build: eager re-walks)
-            h = h0;
-            group_walks_impl<A, true>(S, stk, ro, rd, h, cert);
-        }
-    }
-    if (h.tri >= 0) {  // the winner's barycentrics (for its interpolated normal)
-        const DevObject& ob = S.objs[hit_obj(h)];
-        tri_uv(S.tris[h.ti], xpt<A>(ob.inv, ob.st, ro), xdir<A>(ob.inv, ob.st, rd), h.u, h.v);
-    }
 }
 
 // schlick (tracer.cl:485-505)
@@ -1107,11 +1066,12 @@ __device__ __noinline__ d4 refracted(d4 eye, d4 nrm, double n1, double n2) {
 template <bool A>
 __device__ __forceinline__ d4 reflect(d4 rd, d4 nv) { return sub4(rd, scl4(scl4(nv, 2.0), dotv<A>(rd, nv))); }
 
-// randomVectorInHemisphere (tracer.cl:348-366); x, y, z hold float-valued doubles.
+// randomVectorInHemisphere (tracer.cl:348-366) from its two uniforms
+// u1 = noise3D(x, y, z), u2 = noise3D(y, z, x) (or the statistical mode's draws).
 template <bool A>
-__device__ __forceinline__ d4 random_hemisphere(d4 nv, float fx, float fy, float fz) {
-    double rand1 = 2.0 * kPi * (double)noise3d(fx, fy, fz);
-    double rand2 = (double)noise3d(fy, fz, fx);
+__device__ __forceinline__ d4 random_hemisphere(d4 nv, float u1, float u2) {
+    double rand1 = 2.0 * kPi * (double)u1;
+    double rand2 = (double)u2;
     // Affine: sqrt's core; rand2 is 0 or a float >= 2^-149, so in its range (and 1 - rand2
     // is in (0, 1]), sqrt(+0) = +0 kept by the select.
     double rand2s = A ? (rand2 == 0.0 ? 0.0 : sqrt_core(rand2)) : sqrt(rand2);
@@ -1202,6 +1162,7 @@ struct PathState {
     // sqrt(-0.5), tracer.cl:224) makes every object-space component NaN in the
     // reference (0*NaN = NaN), so it misses everything and the sample adds 0.
     bool dead;
+    Xrng rng;  // statistical mode (F_XRNG) only
 };
 
 // `dead` is a shortcut only (a NaN path misses and adds 0 either way), taken where
@@ -1346,6 +1307,7 @@ __device__ __noinline__ d4 plane_normal_map(const DevTexArray T, const DevObject
 template <int FL>
 __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, const Hit& h, float fgi, uint32_t n) {
     constexpr bool A = !(FL & F_PROJ);
+    constexpr bool kX = (FL & F_XRNG) != 0;
     if (h.pk < 0) return true;  // a miss repeats identically until b == 10 in the reference
     const DevObject& ob = S.objs[h.pk & 0xFFFF];
     const int type = ob.type;
@@ -1404,11 +1366,12 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
     double cosine = 1.0;
     bool entering = false, exiting = false, reflecting = false;
     // Material decision (tracer.cl:973-1061)
-    if ((FL & F_MATERIALS) && ob.reflectivity != 0.0 && noise3d(fgi, (float)n, (float)b) < ob.reflectivity) {
+    if ((FL & F_MATERIALS) && ob.reflectivity != 0.0 &&
+        (kX ? xnext(P.rng) : noise3d(fgi, (float)n, (float)b)) < ob.reflectivity) {
         P.rd = reflect<A>(P.rd, nv);
         reflecting = true;
     } else if ((FL & F_MATERIALS) && ob.refractive_index == -1.0) {
-        if (schlick<A>(eye, nv, 1.0, 1.5) < noise3d(fgi, (float)(n * n), (float)b)) {
+        if (schlick<A>(eye, nv, 1.0, 1.5) < (kX ? xnext(P.rng) : noise3d(fgi, (float)(n * n), (float)b))) {
             over = sub4(pos, scl4(nv, kEps));
         } else {
             P.rd = reflect<A>(P.rd, nv);
@@ -1418,7 +1381,7 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
         const double ri = ob.refractive_index;
         const bool in = P.inside;
         const double sch = in ? schlick<A>(eye, nv, ri, 1.0) : schlick<A>(eye, nv, 1.0, ri);
-        if (sch < noise3d(fgi, (float)(n * n), (float)b)) {
+        if (sch < (kX ? xnext(P.rng) : noise3d(fgi, (float)(n * n), (float)b))) {
             P.rd = in ? refracted<A>(eye, nv, ri, 1.0) : refracted<A>(eye, nv, 1.0, ri);
             over = sub4(pos, scl4(nv, kEps));
             entering = !in;
@@ -1429,7 +1392,15 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
             reflecting = true;
         }
     } else {
-        P.rd = random_hemisphere<A>(nv, fgi, (float)b, (float)n);
+        float u1, u2;
+        if constexpr (kX) {
+            u1 = xnext(P.rng);
+            u2 = xnext(P.rng);
+        } else {
+            u1 = noise3d(fgi, (float)b, (float)n);
+            u2 = noise3d((float)b, (float)n, fgi);
+        }
+        P.rd = random_hemisphere<A>(nv, u1, u2);
         cosine = dotv<A>(P.rd, nv);
     }
     P.ro = over;
@@ -1479,17 +1450,244 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
     return ob.emission[0] > 0.0 || P.b >= kMaxBounces || P.effective >= kMaxEffectiveBounces;
 }
 
-// One wave per workgroup; workgroup b runs work item b of the WorkPlan: an 8x8 tile
-// over the whole sample range (sums -> the frame) or a sample chunk of a tail tile
-// (sums -> its slot of the partial buffer).  RGB sums, A = #samples.
+// ---- Group scenes: walker waves serving a workgroup pool of BVH walk requests -------
+//
+// A group-scene workgroup has kTracers tracer waves, which trace paths exactly like the
+// other scenes' waves, and one walker wave, which does every BVH walk of the group.  A
+// tracer lane whose ray needs a walk (group_needs_walk) parks: the ray and its
+// primitives' best (t, pk) go to the lane's slot of the WalkPool (LDS) and the slot's
+// bit is posted; the lane waits while the wave's other lanes go on tracing.  The walker
+// takes posted requests -- a lane whose walk ends takes the next one (refilled in
+// batches of kRefill lanes) -- so its 64 lanes stay busy while requests wait, instead
+// of a wave stopping to walk its own few parked rays for as long as the longest of them
+// takes (round 2: ~27 of 64 lanes walked per walk phase, for a mean walk of 7.9 of the
+// phase's ~28 steps).  The walker writes the result (t, pk, winning triangle) into the
+// slot and sets its done bit; the owner lane picks it up and shades.  Splitting the
+// roles also splits the registers: a tracer carries no walk state and the walker no
+// path state.  Requests are independent and the closest hit is the lexicographic
+// minimum of the same candidates whoever walks, so images are unchanged; each lane
+// still traces its own samples in order.
+static constexpr int kTL = 64 * kTracers;  // tracer lanes = pool slots
+template <bool A>
+struct WalkPool {
+    static constexpr int kC = A ? 3 : 4;  // ray components kept (affine: no w lanes)
+    double ro[kC][kTL], rd[kC][kTL];      // the parked ray, world space
+    double t[kTL];                        // in: the primitives' best t; out: the walks' best
+    int pk[kTL];                          // in / out: its packed object (pack_hit)
+    int ti[kTL];                          // out: the winning triangle's leaf-order index, or -1
+    unsigned long long posted[kTracers];  // bit l of word w: slot 64 w + l waits for the walker
+    unsigned long long done[kTracers];    // bit l of word w: slot 64 w + l has its result
+    int alive;                            // tracer waves still running
+};
+
+#ifndef PTMI_REFILL_WALKERS
+#define PTMI_REFILL_WALKERS 32  // idle lanes that make a walker stop stepping and take more requests
+#endif
+static constexpr int kRefill = PTMI_REFILL_WALKERS;
+
+__device__ __forceinline__ unsigned long long lds_load64(unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ unsigned long long lds_or64(unsigned long long* p, unsigned long long v) {
+    return __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ unsigned long long lds_and64(unsigned long long* p, unsigned long long v) {
+    return __hip_atomic_fetch_and(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Lanes 0..63 of the wave: popcount of m's bits below this lane.
+__device__ __forceinline__ int rank_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+// Idle walker lanes (req < 0) take posted requests, tracer word `first` first.  Called
+// in wave-uniform control flow with every lane of the wave present.  Per word: the
+// first n set bits of the posted word (n = min(#idle, #posted)) are claimed with one LDS
+// atomic, then the k-th claimed bit goes to the k-th idle lane (two cross-lane
+// permutes); a bit another walker took in between is not received.
+template <bool A>
+__device__ __forceinline__ void claim(WalkPool<A>& Pl, int first, int lane, int& req) {
+    unsigned long long idle = __ballot(req < 0);
+    for (int k = 0; k < kTracers && idle != 0; k++) {
+        const int q = (first + k) % kTracers;
+        const unsigned long long cand = lds_load64(&Pl.posted[q]);
+        if (cand == 0) continue;
+        const int n = min(__popcll(idle), __popcll(cand));
+        const int rb = rank_below(cand);  // rank of bit `lane` among cand's set bits
+        const bool sel = ((cand >> lane) & 1ull) != 0 && rb < n;
+        const unsigned long long want = __ballot(sel);
+        unsigned long long old = 0;
+        if (lane == 0) old = lds_and64(&Pl.posted[q], ~want);
+        const unsigned long long got =
+            kWalkers == 1 ? want
+                          : want & (((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(old >> 32)) << 32) |
+                                    (unsigned)__builtin_amdgcn_readfirstlane((unsigned)old));
+        // Z[r] = the position of the r-th selected bit, held by lane r (push), then the
+        // idle lane of rank r pulls Z[r].  Unselected lanes push to lane 63, which only
+        // matters when n == 64, i.e. when every lane is selected.
+        const int z = __builtin_amdgcn_ds_permute((sel ? rb : 63) * 4, lane);
+        const int ir = rank_below(idle);
+        const int j = __builtin_amdgcn_ds_bpermute(ir * 4, z);
+        if (req < 0 && ir < n && ((got >> j) & 1ull) != 0) req = q * 64 + j;
+        idle = __ballot(req < 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// The walker wave (see WalkPool): serve requests until every tracer wave of the group
+// has left.  Per lane the walks of every group object for one request, unrolled into
+// steps so a lane whose walk ends takes the next request: st 1 = set up the walk of
+// group object `obj` (or move on), 2 = one traversal step (a node or a leaf),
+// 3 = verify and publish the result.  The walks take every Moller-Trumbore hit
+// tentatively: their winner is the minimum over a SUPERSET of the reference's
+// candidates, so if it passes its own gate chain it is the reference's winner.  Only
+// when it fails (seen only with degenerate boxes, tests/adversarial.py) is the request
+// walked again `eager`ly, each improving candidate checked against its gate chain as it
+// is found.
 template <int FL>
+__device__ __forceinline__ void walker_loop(const DevScene& S, WalkPool<!(FL & F_PROJ)>& Pl, int* __restrict__ stk,
+                                            int lane) {
+    constexpr bool A = !(FL & F_PROJ);
+    int req = -1, st = 0;
+    int obj = 0, key = 0, cur = 0, sp = 0, vchain = -1;
+    bool cert = false, eager = false;
+    Hit wh{1024.0, -1, -1, -1, 0.0, 0.0};
+    d4 o{}, d{};
+    float rf[3], ofr[3], dt[3];
+    int rot = (threadIdx.x >> 6) % kTracers;  // the tracer word claimed from first (round robin)
+    auto any_posted = [&]() {
+        unsigned long long m = 0;
+        for (int q = 0; q < kTracers; q++) m |= lds_load64(&Pl.posted[q]);
+        return m != 0;
+    };
+    // Publish a finished request: result into the slot, then its done bit.
+    auto publish = [&]() {
+        if (wh.tri >= 0) PTMI_COUNT(4);  // (stats build: certified winners)
+        Pl.t[req] = wh.t;
+        Pl.pk[req] = wh.pk;
+        Pl.ti[req] = wh.tri >= 0 ? wh.ti : -1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        lds_or64(&Pl.done[req >> 6], 1ull << (req & 63));
+        req = -1;
+        st = 0;
+    };
+    PTMI_TSTAMP(t_wl);
+    for (;;) {
+        PTMI_WADD(23, 1ull);
+        const bool busy = __any(req >= 0);
+        const bool posted = any_posted();
+        if (!busy && !posted) {
+            // A tracer wave leaves only when none of its lanes waits for a walk, so with
+            // every tracer gone no request can appear any more.
+            if (__hip_atomic_load(&Pl.alive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) break;
+            PTMI_TSTAMP(t_sl);
+            __builtin_amdgcn_s_sleep(1);
+            PTMI_WADD(22, 1ull);
+            PTMI_TADD(26, t_sl);
+            continue;
+        }
+        if (posted && __popcll(__ballot(req < 0)) >= (busy ? kRefill : 1)) {
+            const int before = req;
+            claim<A>(Pl, rot, lane, req);
+            rot = rot + 1 == kTracers ? 0 : rot + 1;
+            const bool fresh = req >= 0 && before < 0;
+            PTMI_WADD(24, (unsigned long long)__popcll(__ballot(fresh)));
+            if (fresh) {  // a new request: its primitives' best, the first group object
+                wh = Hit{Pl.t[req], Pl.pk[req], -1, -1, 0.0, 0.0};
+                cert = eager = false;
+                obj = S.run_end[3];
+                st = 1;
+            }
+        }
+        if (st == 1) {  // set up the walk of group object obj (tracer.cl:598-620), or finish
+            if (obj >= S.run_end[4]) {
+                st = 3;
+            } else {
+                const DevObject& ob = S.objs[obj];
+                const d4 wro = mk(Pl.ro[0][req], Pl.ro[1][req], Pl.ro[2][req], A ? 1.0 : Pl.ro[3 % WalkPool<A>::kC][req]);
+                const d4 wrd = mk(Pl.rd[0][req], Pl.rd[1][req], Pl.rd[2][req], A ? 0.0 : Pl.rd[3 % WalkPool<A>::kC][req]);
+                o = xpt<A>(ob.inv, ob.st, wro);
+                d = xdir<A>(ob.inv, ob.st, wrd);
+                const d4 r = mk(rcp_walk(d.x), rcp_walk(d.y), rcp_walk(d.z), 0.0);
+                const RootRec& R = S.root_rec[ob.child_base];  // one traversal index per group object
+                double tn;
+                PTMI_COUNT(7);
+                if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1], R.hull_mx[2],
+                             wh.t + prune_margin(wh.t), tn)) {
+                    obj++;
+                } else {
+                    PTMI_COUNT(0);
+                    walk_setup(o, r, R.bmax, rf, ofr, dt);
+                    key = ob.key;
+                    cur = R.entry;
+                    sp = 0;
+                    vchain = -1;
+                    st = 2;
+                }
+            }
+        }
+        if (st == 3) {  // the deferred gate verification, then publish
+            bool ok = true;
+            if (wh.tri >= 0 && !cert && !eager) {
+                const d4 wro = mk(Pl.ro[0][req], Pl.ro[1][req], Pl.ro[2][req], A ? 1.0 : Pl.ro[3 % WalkPool<A>::kC][req]);
+                const d4 wrd = mk(Pl.rd[0][req], Pl.rd[1][req], Pl.rd[2][req], A ? 0.0 : Pl.rd[3 % WalkPool<A>::kC][req]);
+                const DevObject& ob = S.objs[hit_obj(wh)];
+                ok = verify_chain(S, S.tris[wh.ti].chain, xpt<A>(ob.inv, ob.st, wro), xdir<A>(ob.inv, ob.st, wrd));
+            }
+            if (!ok) {  // walk this request again, eagerly, from its primitives' best
+                PTMI_COUNT(11);  // (stats build: eager re-walks)
+                wh = Hit{Pl.t[req], Pl.pk[req], -1, -1, 0.0, 0.0};
+                eager = true;
+                obj = S.run_end[3];
+                st = 1;
+            } else {
+                publish();
+            }
+        }
+        // Traversal steps of the walking lanes, until enough lanes need a new request
+        // while one is posted, or a lane needs the setup or the verification above.
+        for (;;) {
+            const int n_walk = __popcll(__ballot(st == 2));
+            if (n_walk == 0 || __any(st == 1 || st == 3)) break;
+            if (64 - n_walk >= kRefill && any_posted()) break;
+            PTMI_WADD(19, 1ull);
+            PTMI_WADD(21, (unsigned long long)n_walk);
+            if (st == 2) {  // one step of the walk: a Node4 or a leaf, then pop
+                bool pop = true;
+                if (cur >= 0) {
+                    int next;
+                    if (node_visit(S, stk, cur, sp, rf, ofr, dt, wh.t, next)) {
+                        cur = next;
+                        pop = false;
+                    }
+                } else if (cur != kEmptyChild) {
+                    leaf_visit(S, -cur - 1, obj, key, o, d, wh, vchain, eager);
+                }
+                if (pop) {
+                    if (sp == 0) {  // this object's walk is over: certify a winner from it while its
+                                    // ray is at hand (a later object that takes over re-certifies)
+                        if (!eager && wh.tri >= 0 && hit_obj(wh) == obj)
+                            cert = chain_certified(S, S.tris[wh.ti].chain, o, d, wh.t);
+                        obj++;
+                        if (obj < S.run_end[4]) st = 1;
+                        else if (wh.tri < 0 || cert || eager) publish();  // no verification needed
+                        else st = 3;
+                    } else {
+                        cur = stk[(--sp) * kStkStride];
+                    }
+                }
+            }
+        }
+    }
+    PTMI_TADD(18, t_wl);
+}
+
+// Per-launch resources of trace_kernel<FL>: workgroup size and the register budget.
 #ifndef PTMI_WAVES
 #define PTMI_WAVES 6  // waves/SIMD the register allocation targets (scenes without groups or materials).
-                      // The kernel is VALU-issue bound.  With the sincos constants in SGPRs (ptmi_fp64core.h)
-                      // C2/C3 fit 95 VGPRs at 5 waves without spill (C2 2048 spp 178.0 -> 171.6 ms against
-                      // the old 3-wave budget); 6 waves (80 VGPRs, 64 B/lane of spilled loop invariants)
-                      // gain another 2-2.6 % (C2 171.5 -> 167.9, C3 179.5 -> 174.9 ms); 7 waves (72 VGPRs,
-                      // 96 B/lane) lose 10 %
+                      // With the sincos constants in SGPRs (ptmi_fp64core.h) C2/C3 fit 95 VGPRs at 5 waves
+                      // without spill (C2 2048 spp 178.0 -> 171.6 ms against the old 3-wave budget); 6 waves
+                      // (80 VGPRs, 64 B/lane of spilled loop invariants) gain another 2-2.6 % (C2 171.5 ->
+                      // 167.9, C3 179.5 -> 174.9 ms); 7 waves (72 VGPRs, 96 B/lane) lose 10 %
 #endif
 #ifndef PTMI_WAVES_MATERIALS
 #define PTMI_WAVES_MATERIALS 3  // ... with reflective / refractive materials (at 5 they spill 96-112 B/lane)
@@ -1497,213 +1695,362 @@ template <int FL>
 #ifndef PTMI_WAVES_GROUPS
 #define PTMI_WAVES_GROUPS 3  // ... and with BVH groups (the walk needs more registers; 4 spills)
 #endif
-__global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
-                                    : (FL & F_MATERIALS) ? PTMI_WAVES_MATERIALS
-                                                         : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, WorkPlan WP,
-                                                    const double* __restrict__ seeds, const double* __restrict__ sunf,
-                                                    double* __restrict__ sums, double* __restrict__ part) {
-#if PTMI_STATS
-    if ((threadIdx.x & 63) < 32) ptmi_wstat[threadIdx.x >> 6][threadIdx.x & 63] = 0;
-#endif
-    const int W = S.cam.width, H = S.cam.height;
-    const int tiles_x = (W + kTile - 1) / kTile;
-    const int tiles_y = (H + kTile - 1) / kTile;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // Work item -> (owned tile k, sample range, output slot): WorkPlan.
-    const uint32_t item = blockIdx.x * (kBlock / 64) + wave;
-    uint32_t k, c0, c1;
-    size_t oslot;  // output: pixel index into sums, or slot of the partial buffer
-    bool whole;
-    if (item < WP.n_whole) {
-        whole = true;
-        k = item;
-        c0 = WP.s_begin;
-        c1 = WP.s_end;
-    } else {
-        whole = false;
-        const uint32_t t = item - WP.n_whole;
-        const uint32_t c = t / max(WP.n_tail, 1u), tt = t - c * WP.n_tail;
-        if (c >= WP.nchunks) return;
-        k = WP.n_whole + tt;
-        c0 = WP.s_begin + c * WP.chunk_len;
-        c1 = min(WP.s_end, c0 + WP.chunk_len);
-        oslot = ((size_t)c * WP.n_tail + tt) * 64 + lane;
-    }
-    const uint32_t tile = WP.tile_offset + k * WP.tile_stride;
-    if (tile >= (uint32_t)(tiles_x * tiles_y)) return;
-    const int px0 = (int)(tile % (uint32_t)tiles_x) * kTile + (lane & 7);
-    const int py0 = (int)(tile / (uint32_t)tiles_x) * kTile + (lane >> 3);
-    if (px0 >= W || py0 >= H) return;
+
+// The per-lane sample loop of a tracer wave of a scene with BVH groups (trace_kernel):
+// the loop of the other scenes, with parked lanes waiting for the walker (WalkPool).
+// The pixel's colour sums accumulate in acc_lds.
+template <int FL>
+__device__ __forceinline__ void tracer_loop(const DevScene& S, const double* __restrict__ sunf, WalkPool<!(FL & F_PROJ)>& Pl,
+                                            double* __restrict__ cam_lds, double* __restrict__ acc_lds, int px, int py,
+                                            float fgi, float fgi2, uint64_t seed_bits, uint32_t c0, uint32_t c_end) {
     constexpr bool A = !(FL & F_PROJ);
-    const uint32_t i = (uint32_t)py0 * (uint32_t)W + (uint32_t)px0;
-    if (whole) oslot = i;
-    // fgi / fgi2 (tracer.cl:839-841): double division rounded to float.
-    const double seed = seeds[i];
-    const int px = px0, py = py0;
-    const float fgi = (float)(seed / (double)S.n_list);
-    const float fgi2 = (float)(seed / (double)samples);
-    const uint32_t c_end = c1;
-    double cr = 0.0, cg = 0.0, cb = 0.0;  // colors (tracer.cl:1179)
-    // Group scenes may keep the sums in LDS (one slot per lane, the same additions in the
-    // same order): they change once per path, and the walk phases need the registers.
-    constexpr bool kAccLds = (FL & F_GROUPS) != 0;
-    __shared__ double acc_lds[kAccLds ? 3 * kBlock : 1];
-    if constexpr (kAccLds) {
-        acc_lds[0 * kBlock + threadIdx.x] = 0.0;
-        acc_lds[1 * kBlock + threadIdx.x] = 0.0;
-        acc_lds[2 * kBlock + threadIdx.x] = 0.0;
-    }
-    // Camera rays are produced in wave-wide batches into a kCamDepth-deep per-lane
-    // ring buffer (LDS) and consumed by path regeneration: generating them at the
-    // moment each lane needs one would run the camera block (2 noise3D + the
-    // transform) on nearly every bounce iteration with ~1/5 of the lanes active.
-    // Per lane the samples are still traced in order n = c0, c0+1, ..., so the
-    // arithmetic and the order of `colors +=` are unchanged.
-    // SoA, component c of slot k, lane t at [(k * kCamComp + c) * 256 + t]; affine
-    // scenes keep no w lanes.  Group scenes stay one deep (their LDS holds the
-    // traversal stacks and nodes).
-    constexpr int kCamComp = A ? 6 : 8;
-    constexpr int kCamDepth = 1;  // (2- and 3-deep rings measured no faster on C2, +1.4 % on the group scenes)
-    constexpr int kB = kBlock;  // LDS stride of the per-lane camera slots
-    __shared__ double cam_lds[kCamDepth * kCamComp * kB];
-    const int tid = threadIdx.x;
-    // Per-lane BVH traversal stacks, lane-interleaved (entry k of lane t at
-    // [k * kStkStride + t]) so a wave's pushes and pops hit 64 consecutive dwords.
-    __shared__ int stk_lds[(FL & F_GROUPS) ? kStack * kStkStride : 1];
-    int* stk = (FL & F_GROUPS) ? stk_lds + tid : nullptr;
-    uint32_t n_gen = c0;  // next sample whose camera ray is to be generated
-    uint32_t n_cur = 0;
-    int nb = 0, hb = 0;   // buffered camera rays (samples n_gen - nb ...) and the head slot
-    bool active = false, pending = false;
+    constexpr bool kDof = (FL & F_DOF) != 0;
+    constexpr int kCamComp = (kDof || !A) ? (A ? 6 : 8) : 3;  // without DoF the origin is the camera's
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    uint32_t n_gen = c0, n_cur = 0;
+    bool buffered = false, active = false, pending = false;
     PathState P;
-    // A parked lane's primitive best (t, pk) waits in LDS (group scenes): registers are
-    // what the walk phases need.
-    __shared__ double hp_t_lds[(FL & F_GROUPS) ? kBlock : 1];
-    __shared__ int hp_pk_lds[(FL & F_GROUPS) ? kBlock : 1];
     PTMI_TSTAMP(t_loop);
     for (;;) {
-        if (!__any(active || nb > 0 || n_gen < c_end)) break;
+        if (!__any(active || buffered || n_gen < c_end)) break;
         PTMI_TSTAMP(t_a);
-        const bool need = nb < kCamDepth && n_gen < c_end;
+        // Camera rays in wave-wide batches (see trace_kernel).
+        const bool need = !buffered && n_gen < c_end;
         const int n_need = __popcll(__ballot(need));
-        const int n_starve = __popcll(__ballot(nb == 0 && !active && n_gen < c_end));
-        constexpr int kRefillStarve = (FL & F_GROUPS) ? PTMI_REFILL_STARVE_GROUPS : PTMI_REFILL_STARVE;
-        if (n_need >= kRefillNeed || n_starve >= kRefillStarve || (n_starve > 0 && !__any(active))) {
+        const int n_starve = __popcll(__ballot(!buffered && !active && n_gen < c_end));
+        if (n_need >= kRefillNeed || n_starve >= PTMI_REFILL_STARVE_GROUPS || (n_starve > 0 && !__any(active))) {
             if (need) {
                 d4 ro, rd;
-                ray_for_pixel<(FL & F_DOF) != 0, A>(S.cam, sunf, (unsigned)px, (unsigned)py,
-                                                    noise3d(fgi, (float)n_gen, fgi2), noise3d(fgi, fgi2, (float)n_gen),
-                                                    (int)n_gen, ro, rd);
-                int slot = hb + nb;
-                if (slot >= kCamDepth) slot -= kCamDepth;
-                double* cb = cam_lds + slot * (kCamComp * kB) + tid;
-                cb[0 * kB] = ro.x;
-                cb[1 * kB] = ro.y;
-                cb[2 * kB] = ro.z;
-                cb[3 * kB] = rd.x;
-                cb[4 * kB] = rd.y;
-                cb[5 * kB] = rd.z;
+                float rx, ry;
+                camera_offsets<FL>(fgi, fgi2, seed_bits, n_gen, rx, ry);
+                ray_for_pixel<kDof, A>(S.cam, sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n_gen, ro, rd);
+                double* cb = cam_lds + tid;
+                cb[0 * kTL] = rd.x;
+                cb[1 * kTL] = rd.y;
+                cb[2 * kTL] = rd.z;
+                if constexpr (kCamComp > 3) {
+                    cb[3 * kTL] = ro.x;
+                    cb[4 * kTL] = ro.y;
+                    cb[5 * kTL] = ro.z;
+                }
                 if constexpr (!A) {
-                    cb[6 * kB] = ro.w;
-                    cb[7 * kB] = rd.w;
+                    cb[6 * kTL] = ro.w;
+                    cb[7 * kTL] = rd.w;
                 }
                 n_gen++;
-                nb++;
+                buffered = true;
             }
         }
-        if (!active && nb > 0) {
-            const double* cb = cam_lds + hb * (kCamComp * kB) + tid;
-            const d4 cro = mk(cb[0 * kB], cb[1 * kB], cb[2 * kB], A ? 1.0 : cb[6 * kB]);
-            const d4 crd = mk(cb[3 * kB], cb[4 * kB], cb[5 * kB], A ? 0.0 : cb[7 * kB]);
-            start_path<A, (FL & F_DOF) != 0>(P, cro, crd);
-            n_cur = n_gen - (uint32_t)nb;
-            hb = (hb + 1 == kCamDepth) ? 0 : hb + 1;
-            nb--;
+        if (!active && buffered) {
+            const double* cb = cam_lds + tid;
+            const d4 crd = mk(cb[0 * kTL], cb[1 * kTL], cb[2 * kTL], A ? 0.0 : cb[(kCamComp - 1) * kTL]);
+            d4 cro;
+            if constexpr (kCamComp > 3)
+                cro = mk(cb[3 * kTL], cb[4 * kTL], cb[5 * kTL], A ? 1.0 : cb[(kCamComp - 2) * kTL]);
+            else
+                cro = mk(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], 1.0);  // ray_for_pixel's origin
+            start_path<A, kDof>(P, cro, crd);
+            n_cur = n_gen - 1;
+            if constexpr ((FL & F_XRNG) != 0) P.rng = xseed(seed_bits, n_cur);
+            buffered = false;
             active = true;
         }
         PTMI_TADD(12, t_a);
+        // Walk results for this wave's parked lanes; when every active lane is parked and
+        // no result has come, the wave yields its issue slots to the walker for a while.
+        PTMI_TSTAMP(t_c);
+        bool walked = false;
+        const unsigned long long out = __ballot(pending);
+        if (out != 0) {
+            const unsigned long long got = out & lds_load64(&Pl.done[wave]);
+            if (got != 0) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                walked = pending && ((got >> lane) & 1ull) != 0;
+                if (lane == 0) lds_and64(&Pl.done[wave], ~got);
+            } else if (!__any(active && !pending)) {
+                PTMI_WADD(8, 1ull);
+                __builtin_amdgcn_s_sleep(1);
+                PTMI_TADD(14, t_c);
+                continue;
+            }
+        }
+        PTMI_TADD(14, t_c);
         PTMI_TSTAMP(t_b);
-        // Closest hit.  Scenes with BVH groups defer the walks: a lane whose ray
-        // needs one parks (pending, keeping its primitives' best in hp) and the
-        // wave walks all parked lanes together once kWalkBatch are parked or no
-        // lane is ready to shade -- a walk costs the whole wave its longest
-        // traversal, so it should run with many lanes, not the ~10 % of rays
-        // that reach a mesh in any one bounce.  Each lane still traces its
-        // samples in order, and the closest hit does not depend on when or in
-        // which order candidates are examined (lexicographic minimum, better()).
         bool ready = false;
         Hit h;
-#if PTMI_STATS
-        PTMI_WADD(10, 1ull);
-        PTMI_WADD(26, (unsigned long long)__popcll(__ballot(!active && (nb > 0 || n_gen < c_end))));
-        PTMI_WADD(27, (unsigned long long)__popcll(__ballot(!active && nb == 0 && n_gen >= c_end)));
-        PTMI_WADD(28, (unsigned long long)__popcll(__ballot(active && !pending)));
-#endif
-        if (active && !pending) {
+        if (walked) {  // the walks' closest hit: (t, pk) and the winning triangle's barycentrics
+            pending = false;
+            ready = true;
+            P.ro = mk(Pl.ro[0][tid], Pl.ro[1][tid], Pl.ro[2][tid], A ? 1.0 : Pl.ro[3 % WalkPool<A>::kC][tid]);
+            P.rd = mk(Pl.rd[0][tid], Pl.rd[1][tid], Pl.rd[2][tid], A ? 0.0 : Pl.rd[3 % WalkPool<A>::kC][tid]);
+            h = Hit{Pl.t[tid], Pl.pk[tid], -1, -1, 0.0, 0.0};
+            const int ti = Pl.ti[tid];
+            if (ti >= 0) {
+                const DevTri& T = S.tris[ti];
+                const DevObject& ob = S.objs[hit_obj(h)];
+                h.ti = ti;
+                h.tri = T.n;
+                tri_uv(T, xpt<A>(ob.inv, ob.st, P.ro), xdir<A>(ob.inv, ob.st, P.rd), h.u, h.v);
+            }
+        } else if (active && !pending) {
             if (P.dead) {
                 h.pk = -1;
                 ready = true;
             } else {
                 h = find_closest_prims<FL>(S, P.ro, P.rd);
-                if ((FL & F_GROUPS) && group_needs_walk<A>(S, P.ro, P.rd, h)) {
+                if (group_needs_walk<A>(S, P.ro, P.rd, h)) {  // park: post the ray to the pool
                     pending = true;
-                    hp_t_lds[threadIdx.x] = h.t;  // find_closest_prims: tri, ti, u, v are constants
-                    hp_pk_lds[threadIdx.x] = h.pk;
+                    Pl.ro[0][tid] = P.ro.x;
+                    Pl.ro[1][tid] = P.ro.y;
+                    Pl.ro[2][tid] = P.ro.z;
+                    Pl.rd[0][tid] = P.rd.x;
+                    Pl.rd[1][tid] = P.rd.y;
+                    Pl.rd[2][tid] = P.rd.z;
+                    if constexpr (!A) {
+                        Pl.ro[3 % WalkPool<A>::kC][tid] = P.ro.w;
+                        Pl.rd[3 % WalkPool<A>::kC][tid] = P.rd.w;
+                    }
+                    Pl.t[tid] = h.t;  // find_closest_prims: tri, ti, u, v are constants
+                    Pl.pk[tid] = h.pk;
                 } else {
                     ready = true;
                 }
             }
         }
-        PTMI_TADD(13, t_b);
-        PTMI_TSTAMP(t_c);
-        if (FL & F_GROUPS) {
-            const int n_pend = __popcll(__ballot(pending));
-            if (n_pend >= kWalkBatch || (n_pend > 0 && !__any(ready))) {
-                PTMI_WADD(8, 1ull);
-                PTMI_WADD(9, (unsigned long long)n_pend);
-                if (pending) {
-                    h = Hit{hp_t_lds[threadIdx.x], hp_pk_lds[threadIdx.x], -1, -1, 0.0, 0.0};
-                    group_walks<A>(S, stk, P.ro, P.rd, h);
-                    pending = false;
-                    ready = true;
-                }
-            }
+        const unsigned long long posts = __ballot(pending) & ~out;
+        if (posts != 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) lds_or64(&Pl.posted[wave], posts);
         }
-        PTMI_TADD(14, t_c);
-        PTMI_WADD(24, (unsigned long long)__popcll(__ballot(ready)));
-        PTMI_WADD(25, (unsigned long long)__popcll(__ballot(pending)));
+        PTMI_TADD(13, t_b);
         PTMI_TSTAMP(t_d);
         if (ready && bounce_shade<FL>(S, P, h, fgi, n_cur)) {
-            if constexpr (kAccLds) {
-                double* a = acc_lds + threadIdx.x;
-                a[0 * kBlock] = a[0 * kBlock] + P.ar;
-                a[1 * kBlock] = a[1 * kBlock] + P.ag;
-                a[2 * kBlock] = a[2 * kBlock] + P.ab;
-            } else {
-                cr = cr + P.ar;  // colors += accumColor (tracer.cl:1179)
-                cg = cg + P.ag;
-                cb = cb + P.ab;
-            }
+            double* a = acc_lds + tid;  // colors += accumColor (tracer.cl:1179), kept in LDS
+            a[0 * kTL] = a[0 * kTL] + P.ar;
+            a[1 * kTL] = a[1 * kTL] + P.ag;
+            a[2 * kTL] = a[2 * kTL] + P.ab;
             active = false;
         }
         PTMI_TADD(15, t_d);
+        PTMI_WADD(10, 1ull);
     }
     PTMI_TADD(16, t_loop);
-#if PTMI_STATS
-    if (PTMI_FIRST_ACTIVE())
-        for (int k = 0; k < 32; k++)
-            if (ptmi_wstat[threadIdx.x >> 6][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[threadIdx.x >> 6][k]);
-#endif
-    if constexpr (kAccLds) {
-        cr = acc_lds[0 * kBlock + threadIdx.x];
-        cg = acc_lds[1 * kBlock + threadIdx.x];
-        cb = acc_lds[2 * kBlock + threadIdx.x];
+}
+
+// Work item of a wave (WorkPlan): the tile's pixel of this lane, its sample range and
+// where its sums go.  ok == false: the wave has no item.
+struct Item {
+    bool ok, whole, inside;
+    uint32_t c0, c1;
+    size_t oslot;  // output: pixel index into sums, or slot of the partial buffer
+    uint32_t i;    // pixel index (inside only)
+    int px, py;
+};
+__device__ __forceinline__ Item work_item(const DevScene& S, const WorkPlan& WP, uint32_t item, int lane) {
+    Item it{};
+    const int W = S.cam.width, H = S.cam.height;
+    const int tiles_x = (W + kTile - 1) / kTile;
+    const int tiles_y = (H + kTile - 1) / kTile;
+    uint32_t k;
+    if (item < WP.n_whole) {
+        it.whole = true;
+        k = item;
+        it.c0 = WP.s_begin;
+        it.c1 = WP.s_end;
+    } else {
+        it.whole = false;
+        const uint32_t t = item - WP.n_whole;
+        const uint32_t c = t / max(WP.n_tail, 1u), tt = t - c * WP.n_tail;
+        if (c >= WP.nchunks) return it;
+        k = WP.n_whole + tt;
+        it.c0 = WP.s_begin + c * WP.chunk_len;
+        it.c1 = min(WP.s_end, it.c0 + WP.chunk_len);
+        it.oslot = ((size_t)c * WP.n_tail + tt) * 64 + lane;
     }
-    double* o = (whole ? sums : part) + oslot * 4;
+    const uint32_t tile = WP.tile_offset + k * WP.tile_stride;
+    if (tile >= (uint32_t)(tiles_x * tiles_y)) return it;
+    it.px = (int)(tile % (uint32_t)tiles_x) * kTile + (lane & 7);
+    it.py = (int)(tile / (uint32_t)tiles_x) * kTile + (lane >> 3);
+    // A lane outside the image (edge tiles) stays in its wave's loop without samples:
+    // the walk pool's cross-lane steps need every lane of the wave.
+    it.inside = it.px < W && it.py < H;
+    it.i = it.inside ? (uint32_t)it.py * (uint32_t)W + (uint32_t)it.px : 0u;
+    if (it.whole) it.oslot = it.i;
+    it.ok = true;
+    return it;
+}
+
+__device__ __forceinline__ void store_sums(const Item& it, double* __restrict__ sums, double* __restrict__ part, double cr,
+                                           double cg, double cb) {
+    if (!it.inside) return;
+    double* o = (it.whole ? sums : part) + it.oslot * 4;
     o[0] = cr;
     o[1] = cg;
     o[2] = cb;
-    o[3] = (double)(c1 > c0 ? c1 - c0 : 0);
+    o[3] = (double)(it.c1 > it.c0 ? it.c1 - it.c0 : 0);
+}
+
+// trace_kernel's body for scenes with BVH groups: kTracers tracer waves and one walker
+// wave per workgroup, sharing the walk pool, the walker's traversal stacks and the
+// tracers' camera buffers and colour sums in LDS.
+template <int FL>
+__device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples, const WorkPlan& WP,
+                                             const double* __restrict__ seeds, const double* __restrict__ sunf,
+                                             double* __restrict__ sums, double* __restrict__ part) {
+    constexpr bool A = !(FL & F_PROJ);
+    constexpr int kCamComp = ((FL & F_DOF) || !A) ? (A ? 6 : 8) : 3;
+    __shared__ WalkPool<A> pool;
+    __shared__ int stk_lds[kWalkers * kStack * kStkStride];
+    __shared__ double acc_lds[3 * kTL];
+    __shared__ double cam_lds[kCamComp * kTL];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    if (tid < kTracers) {  // before any wave can leave
+        pool.posted[tid] = 0;
+        pool.done[tid] = 0;
+    }
+    if (tid == 0) pool.alive = kTracers;
+    __syncthreads();
+#if PTMI_STATS
+    if (lane < 32) ptmi_wstat[wave][lane] = 0;
+#endif
+    if (wave >= kTracers) {  // a walker
+        walker_loop<FL>(S, pool, stk_lds + (wave - kTracers) * kStack * kStkStride + lane, lane);
+    } else {
+        const Item it = work_item(S, WP, blockIdx.x * kTracers + wave, lane);
+        if (it.ok) {
+            // fgi / fgi2 (tracer.cl:839-841): double division rounded to float.
+            const double seed = it.inside ? seeds[it.i] : 0.0;
+            const float fgi = (float)(seed / (double)S.n_list);
+            const float fgi2 = (float)(seed / (double)samples);
+            acc_lds[0 * kTL + tid] = 0.0;
+            acc_lds[1 * kTL + tid] = 0.0;
+            acc_lds[2 * kTL + tid] = 0.0;
+            tracer_loop<FL>(S, sunf, pool, cam_lds, acc_lds, it.px, it.py, fgi, fgi2,
+                            (uint64_t)__double_as_longlong(seed), it.c0, it.inside ? it.c1 : it.c0);
+            store_sums(it, sums, part, acc_lds[0 * kTL + tid], acc_lds[1 * kTL + tid], acc_lds[2 * kTL + tid]);
+        }
+        if (lane == 0) __hip_atomic_fetch_add(&pool.alive, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+#if PTMI_STATS
+    if (PTMI_FIRST_ACTIVE())
+        for (int k = 0; k < 32; k++)
+            if (ptmi_wstat[wave][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[wave][k]);
+#endif
+}
+
+// Workgroup b runs work items b * w .. b * w + w - 1 of the WorkPlan (w waves per group:
+// Launch<FL>): an 8x8 tile over the whole sample range (sums -> the frame) or a sample
+// chunk of a tail tile (sums -> its slot of the partial buffer).  RGB sums, A = #samples.
+template <int FL>
+__global__ __launch_bounds__(Launch<FL>::threads, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
+                                                  : (FL & F_MATERIALS) ? PTMI_WAVES_MATERIALS
+                                                                       : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, WorkPlan WP,
+                                                    const double* __restrict__ seeds, const double* __restrict__ sunf,
+                                                    double* __restrict__ sums, double* __restrict__ part) {
+    if constexpr ((FL & F_GROUPS) != 0) {
+        trace_groups<FL>(S, samples, WP, seeds, sunf, sums, part);
+    } else {
+        constexpr bool A = !(FL & F_PROJ);
+        const int tid = threadIdx.x, lane = tid & 63;
+#if PTMI_STATS
+        if (lane < 32) ptmi_wstat[0][lane] = 0;
+#endif
+        const Item it = work_item(S, WP, blockIdx.x, lane);
+        if (!it.ok) return;
+        const int px = it.px, py = it.py;
+        // fgi / fgi2 (tracer.cl:839-841): double division rounded to float.
+        const double seed = it.inside ? seeds[it.i] : 0.0;
+        const float fgi = (float)(seed / (double)S.n_list);
+        const float fgi2 = (float)(seed / (double)samples);
+        const uint64_t seed_bits = (uint64_t)__double_as_longlong(seed);
+        const uint32_t c_end = it.inside ? it.c1 : it.c0;
+        double cr = 0.0, cg = 0.0, cb = 0.0;  // colors (tracer.cl:1179)
+        // Camera rays are produced in wave-wide batches into a one-deep per-lane buffer
+        // (LDS) and consumed by path regeneration: generating them at the moment each lane
+        // needs one would run the camera block (2 noise3D + the transform) on nearly every
+        // bounce iteration with ~1/5 of the lanes active.  Per lane the samples are still
+        // traced in order n = c0, c0+1, ..., so the arithmetic and the order of `colors +=`
+        // are unchanged.  SoA, component c of lane t at [c * 64 + t]: the direction, then
+        // (DoF or non-affine scenes) the origin; affine scenes keep no w lanes.  (2- and
+        // 3-deep buffers measured no faster on C2, +1.4 % on the group scenes.)
+        constexpr int kCamComp = ((FL & F_DOF) || !A) ? (A ? 6 : 8) : 3;
+        constexpr int kWg = kBlock;
+        __shared__ double cam_lds[kCamComp * kWg];
+        uint32_t n_gen = it.c0;  // next sample whose camera ray is to be generated
+        uint32_t n_cur = 0;
+        bool buffered = false, active = false;
+        PathState P;
+        PTMI_TSTAMP(t_loop);
+        for (;;) {
+            if (!__any(active || buffered || n_gen < c_end)) break;
+            PTMI_TSTAMP(t_a);
+            const bool need = !buffered && n_gen < c_end;
+            const int n_need = __popcll(__ballot(need));
+            const int n_starve = __popcll(__ballot(!buffered && !active && n_gen < c_end));
+            if (n_need >= kRefillNeed || n_starve >= PTMI_REFILL_STARVE || (n_starve > 0 && !__any(active))) {
+                if (need) {
+                    d4 ro, rd;
+                    float rx, ry;
+                    camera_offsets<FL>(fgi, fgi2, seed_bits, n_gen, rx, ry);
+                    ray_for_pixel<(FL & F_DOF) != 0, A>(S.cam, sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n_gen,
+                                                        ro, rd);
+                    double* cbuf = cam_lds + tid;
+                    cbuf[0 * kWg] = rd.x;
+                    cbuf[1 * kWg] = rd.y;
+                    cbuf[2 * kWg] = rd.z;
+                    if constexpr (kCamComp > 3) {
+                        cbuf[3 * kWg] = ro.x;
+                        cbuf[4 * kWg] = ro.y;
+                        cbuf[5 * kWg] = ro.z;
+                    }
+                    if constexpr (!A) {
+                        cbuf[6 * kWg] = ro.w;
+                        cbuf[7 * kWg] = rd.w;
+                    }
+                    n_gen++;
+                    buffered = true;
+                }
+            }
+            if (!active && buffered) {
+                const double* cbuf = cam_lds + tid;
+                const d4 crd = mk(cbuf[0 * kWg], cbuf[1 * kWg], cbuf[2 * kWg], A ? 0.0 : cbuf[(kCamComp - 1) * kWg]);
+                d4 cro;
+                if constexpr (kCamComp > 3)
+                    cro = mk(cbuf[3 * kWg], cbuf[4 * kWg], cbuf[5 * kWg], A ? 1.0 : cbuf[(kCamComp - 2) * kWg]);
+                else
+                    cro = mk(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], 1.0);  // ray_for_pixel's origin
+                start_path<A, (FL & F_DOF) != 0>(P, cro, crd);
+                n_cur = n_gen - 1;
+                if constexpr ((FL & F_XRNG) != 0) P.rng = xseed(seed_bits, n_cur);
+                buffered = false;
+                active = true;
+            }
+            PTMI_TADD(12, t_a);
+            PTMI_TSTAMP(t_b);
+            Hit h;
+            if (active) {
+                if (P.dead) h.pk = -1;
+                else h = find_closest_prims<FL>(S, P.ro, P.rd);
+            }
+            PTMI_TADD(13, t_b);
+            PTMI_TSTAMP(t_d);
+            if (active && bounce_shade<FL>(S, P, h, fgi, n_cur)) {
+                cr = cr + P.ar;  // colors += accumColor (tracer.cl:1179)
+                cg = cg + P.ag;
+                cb = cb + P.ab;
+                active = false;
+            }
+            PTMI_TADD(15, t_d);
+            PTMI_WADD(10, 1ull);
+        }
+        PTMI_TADD(16, t_loop);
+#if PTMI_STATS
+        if (PTMI_FIRST_ACTIVE())
+            for (int k = 0; k < 32; k++)
+                if (ptmi_wstat[0][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[0][k]);
+#endif
+        store_sums(it, sums, part, cr, cg, cb);
+    }
 }
 
 // DoF aperture offsets sunflower(S, 2, n) for n in [0, S) (tracer.cl:221-248,
@@ -1814,16 +2161,24 @@ __global__ __launch_bounds__(256) void seeds_kernel(double* __restrict__ seeds, 
 }
 
 // ---- host-side launch wrappers (called from ptmi_api.cpp) ----------------------
-int trace_block_threads(int flags) { return kBlock; }
-int trace_tiles_per_block(int flags) { return kBlock / 64; }
+int trace_block_threads(int flags) { return (flags & F_GROUPS) ? kGB : kBlock; }
+int trace_tiles_per_block(int flags) { return (flags & F_GROUPS) ? kTracers : 1; }  // waves with work items
+
+// The instantiation a scene's flags launch: textured and non-affine scenes take the
+// generic ones; F_XRNG exists for the affine instantiations (ptmi_scene_set_rng).
+static int kernel_flags(int flags) {
+    if (flags & F_TEX) return F_ALL | F_PROJ | F_TEX;
+    if (flags & F_PROJ) return F_ALL | F_PROJ;
+    return flags & (F_ALL | F_XRNG);
+}
 
 const void* trace_kernel_symbol(int flags) {
-    if (flags & F_TEX) return reinterpret_cast<const void*>(&trace_kernel<F_ALL | F_PROJ | F_TEX>);
-    if (flags & F_PROJ) return reinterpret_cast<const void*>(&trace_kernel<F_ALL | F_PROJ>);
-    switch (flags & F_ALL) {
+    switch (kernel_flags(flags)) {
 #define K(f) \
     case f: return reinterpret_cast<const void*>(&trace_kernel<f>);
         K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15)
+        K(F_ALL | F_PROJ) K(F_ALL | F_PROJ | F_TEX)
+        K(64) K(65) K(66) K(67) K(68) K(69) K(70) K(71) K(72) K(73) K(74) K(75) K(76) K(77) K(78) K(79)
 #undef K
     }
     return nullptr;
@@ -1831,27 +2186,22 @@ const void* trace_kernel_symbol(int flags) {
 
 hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const double* seeds,
                         const double* sunf, double* sums, double* part, hipStream_t st) {
-    constexpr int wpb = kBlock / 64;
     const uint32_t items = WP.n_whole + WP.n_tail * WP.nchunks;
     if (items == 0) return hipSuccess;
-    const dim3 grid((items + wpb - 1) / wpb);
-    if (flags & F_TEX) {  // textured scene: the generic instantiation plus the texture lookups
-        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ | F_TEX>, grid, dim3(kBlock), 0, st, S, samples, WP, seeds, sunf,
-                           sums, part);
-        return hipGetLastError();
-    }
-    if (flags & F_PROJ) {  // non-affine scene: one generic instantiation with the literal w arithmetic
-        hipLaunchKernelGGL(trace_kernel<F_ALL | F_PROJ>, grid, dim3(kBlock), 0, st, S, samples, WP, seeds, sunf, sums,
-                           part);
-        return hipGetLastError();
-    }
-    switch (flags & F_ALL) {
-#define K(f)                                                                                                  \
-    case f:                                                                                                   \
-        hipLaunchKernelGGL(trace_kernel<f>, grid, dim3(kBlock), 0, st, S, samples, WP, seeds, sunf, sums, part); \
+    flags = kernel_flags(flags);
+    const int threads = trace_block_threads(flags), wpb = trace_tiles_per_block(flags);
+    const dim3 grid((items + wpb - 1) / wpb), block(threads);
+    switch (flags) {
+#define K(f)                                                                                          \
+    case f:                                                                                           \
+        hipLaunchKernelGGL(trace_kernel<f>, grid, block, 0, st, S, samples, WP, seeds, sunf, sums, part); \
         break;
         K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15)
+        K(F_ALL | F_PROJ) K(F_ALL | F_PROJ | F_TEX)
+        K(64) K(65) K(66) K(67) K(68) K(69) K(70) K(71) K(72) K(73) K(74) K(75) K(76) K(77) K(78) K(79)
 #undef K
+    default:
+        return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }

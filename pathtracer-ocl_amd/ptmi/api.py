@@ -24,11 +24,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTMI_LIB", os.path.join(_HERE, "..", "build", "libptmi.so"))
 
 PTMI_OK, PTMI_ERR_ARG, PTMI_ERR_DEVICE, PTMI_ERR_HIP, PTMI_ERR_UNSUPPORTED, PTMI_ERR_NOMEM = 0, -1, -2, -3, -4, -5
+RNG_NOISE3D, RNG_XOSHIRO = 0, 1  # ptmi_scene_set_rng: parity (default) / opt-in statistical mode
 
 EXPORTS = ("ptmi_trace", "ptmi_device_count", "ptmi_device_name", "ptmi_scene_create", "ptmi_scene_destroy",
            "ptmi_scene_size", "ptmi_scene_render", "ptmi_finalize", "ptmi_fill_seeds", "ptmi_build_info",
            "ptmi_scene_set_timing", "ptmi_scene_kernel_time", "ptmi_trace_multi", "ptmi_scene_create_textured",
-           "ptmi_trace_multi_timed", "ptmi_sample_split_point", "ptmi_combine_frames")
+           "ptmi_trace_multi_timed", "ptmi_sample_split_point", "ptmi_combine_frames",
+           "ptmi_scene_set_rng")
 
 
 class MultiTiming(ctypes.Structure):
@@ -69,8 +71,9 @@ def load_library(path=None):
     lib.ptmi_trace_multi_timed.restype = i32
     lib.ptmi_trace_multi_timed.argtypes = [vp, u32, vp, u32, vp, u32, vp, u32, i32, u32, vp, vp, ctypes.c_uint64, vp,
                                            vp, ctypes.POINTER(MultiTiming), cp, sz]
-    lib.ptmi_combine_frames.restype = i32
-    lib.ptmi_combine_frames.argtypes = [vp, u32, u32, vp, u32, vp, cp, sz]
+    if hasattr(lib, "ptmi_combine_frames"):
+        lib.ptmi_combine_frames.restype = i32
+        lib.ptmi_combine_frames.argtypes = [vp, u32, u32, vp, u32, vp, cp, sz]
     lib.ptmi_sample_split_point.restype = u32
     lib.ptmi_sample_split_point.argtypes = [i32, i32, u32]
     lib.ptmi_device_count.restype = i32
@@ -91,6 +94,9 @@ def load_library(path=None):
     lib.ptmi_finalize.argtypes = [vp, vp, u32, u32, vp, cp, sz]
     lib.ptmi_fill_seeds.restype = i32
     lib.ptmi_fill_seeds.argtypes = [vp, u32, ctypes.c_uint64, vp, cp, sz]
+    if hasattr(lib, "ptmi_scene_set_rng"):  # (older diagnostic builds lack it; tests/test_abi.py checks the product)
+        lib.ptmi_scene_set_rng.restype = i32
+        lib.ptmi_scene_set_rng.argtypes = [vp, i32, cp, sz]
     lib.ptmi_scene_set_timing.restype = i32
     lib.ptmi_scene_set_timing.argtypes = [vp, i32]
     lib.ptmi_scene_kernel_time.restype = i32
@@ -234,6 +240,12 @@ class Scene:
         rc = self._lib.ptmi_finalize(ctypes.c_void_p(sums_ptr), ctypes.c_void_p(out_ptr),
                                      self.width * self.height, samples, ctypes.c_void_p(stream), err, len(err))
         _check(rc, err)
+
+    def set_rng(self, mode):
+        """RNG_NOISE3D (default, the reference's noise3D bit for bit) or RNG_XOSHIRO (the
+        opt-in statistical mode: images converge to the same expectation, not equal)."""
+        err = ctypes.create_string_buffer(256)
+        _check(self._lib.ptmi_scene_set_rng(self._h, int(mode), err, len(err)), err)
 
     def set_timing(self, enable=True):
         self._lib.ptmi_scene_set_timing(self._h, 1 if enable else 0)
