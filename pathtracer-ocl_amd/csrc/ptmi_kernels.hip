@@ -43,12 +43,12 @@ __device__ unsigned long long ptmi_stats[40];
 // Per-wave accumulators (one writer per wave: the first active lane), flushed to
 // ptmi_stats with one atomic per counter when the wave leaves its loop, so clock
 // and per-wave counts do not serialise on global atomics.
-__shared__ unsigned long long ptmi_wstat[8][32];
+__shared__ unsigned long long ptmi_wstat[1][32];
 #define PTMI_FIRST_ACTIVE() ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1)
 #define PTMI_WADD(i, v)                                                \
     do {                                                               \
         const unsigned long long v_ = (v);                             \
-        if (PTMI_FIRST_ACTIVE()) ptmi_wstat[threadIdx.x >> 6][i] += v_; \
+        if (PTMI_FIRST_ACTIVE()) ptmi_wstat[0][i] += v_;                   \
     } while (0)
 #if PTMI_STATS == 2
 #define PTMI_COUNT(i) ((void)0)
@@ -88,6 +88,10 @@ static constexpr double kPi = (double)3.14159265359f;  // tracer.cl:1 (a float l
 #define PTMI_REFILL_STARVE_GROUPS 12
 #endif
 static constexpr int kRefillNeed = PTMI_REFILL_NEED;
+#ifndef PTMI_WALK_BATCH
+#define PTMI_WALK_BATCH 24
+#endif
+static constexpr int kWalkBatch = PTMI_WALK_BATCH;  // parked lanes that trigger a wave's BVH walk phase
 
 struct d4 {
     double x, y, z, w;
@@ -396,27 +400,8 @@ __device__ __forceinline__ void camera_offsets(float fgi, float fgi2, uint64_t s
 // 189.0 -> 177.1 ms, C2 236.0 -> 235.3 ms per 2048 spp).  BVH scenes then stage
 // only the top 3 levels of the traversal index per group (kLdsNodes).
 static constexpr int kBlock = 64;
-// Scenes with BVH groups run workgroups of kTracers tracer waves and kWalkers walker
-// waves sharing a pool of BVH walk requests in LDS (WalkPool); the other scenes one
-// wave per group.
-#ifndef PTMI_TRACERS
-#define PTMI_TRACERS 3
-#endif
-#ifndef PTMI_WALKERS
-#define PTMI_WALKERS 1
-#endif
-static constexpr int kTracers = PTMI_TRACERS;  // tracer waves per group workgroup
-static constexpr int kWalkers = PTMI_WALKERS;  // walker waves per group workgroup
-static constexpr int kGroupWaves = kTracers + kWalkers;
-static constexpr int kGB = 64 * kGroupWaves;
-static_assert(kTracers >= 1 && kWalkers >= 1 && kGroupWaves <= 8, "tracers and walkers per group");
-template <int FL>
-struct Launch {
-    static constexpr int threads = (FL & 1) ? kGB : kBlock;  // FL & F_GROUPS
-};
-// The walker's per-lane traversal stacks are lane-interleaved: entry k of lane t at
-// [k * kStkStride + t].
-static constexpr int kStkStride = 64;
+// Per-lane traversal stacks are lane-interleaved: entry k of lane t at [k * kStkStride + t].
+static constexpr int kStkStride = kBlock;
 
 
 // intersectRayWithBox (tracer.cl:270-280) returning the line's slab interval.
@@ -492,8 +477,9 @@ __device__ __forceinline__ bool ray_box_ref(d4 o, d4 d, d4 r, const double* mn, 
 __device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o, d4 d);
 __device__ __forceinline__ bool chain_certified(const DevScene& S, int chain, d4 o, d4 d, double t);
 
+template <bool kVerify>
 __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, int ti, d4 o, d4 d, int slot, int key,
-                                         Hit& h, int& vchain, bool verify) {
+                                         Hit& h, int& vchain) {
     const double e1x = T.e1[0], e1y = T.e1[1], e1z = T.e1[2];
     const double e2x = T.e2[0], e2y = T.e2[1], e2z = T.e2[2];
     // dirCrossE2 = cross(d, e2)
@@ -529,9 +515,9 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, int
         const int c = T.chain;
         // Eager mode admits the hit only if the reference would have tested this
         // triangle: its gate chain (root -> its node) passes the exact line-box
-        // tests.  The fast mode takes it tentatively; walker_loop verifies the
+        // tests.  The fast mode takes it tentatively; group_walks verifies the
         // final winner.
-        if (verify && c != vchain) {
+        if (kVerify && c != vchain) {
             if (!chain_certified(S, c, o, d, t) && !verify_chain(S, c, o, d)) {
                 PTMI_COUNT(5);  // (stats build: gate rejections)
                 return;
@@ -712,15 +698,60 @@ __device__ __forceinline__ bool node_visit(const DevScene& S, int* __restrict__ 
 }
 
 // The triangles of one leaf (code = first << 3 | count).
+template <bool kVerify>
 __device__ __forceinline__ void leaf_visit(const DevScene& S, int code, int slot, int key, d4 o, d4 d, Hit& h,
-                                           int& vchain, bool verify) {
+                                           int& vchain) {
     PTMI_WADD(31, 1ull);
     const int first = code >> 3, end = first + (code & 7);
     PTMI_COUNT(2);
     for (int i = first; i < end; i++) {
         PTMI_COUNT(3);
-        tri_test(S, S.tris[i], i, o, d, slot, key, h, vchain, verify);
+        tri_test<kVerify>(S, S.tris[i], i, o, d, slot, key, h, vchain);
     }
+}
+
+// Closest-hit walk of one root's 4-wide traversal index (ptmi_bvh.cpp): nearest
+// child first, the others pushed far-to-near.  Which triangles are FOUND does
+// not depend on the visiting order or the widened boxes (every triangle that
+// can produce a winning t is reached); ties resolve through better_tri.
+template <bool kVerify>
+__device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const RootRec& R, int slot,
+                                           int key, d4 o, d4 d, d4 rw, Hit& h, int& vchain) {
+    float rf[3], ofr[3], dt[3];  // FP32 slab tests (walk_setup)
+    walk_setup(o, rw, R.bmax, rf, ofr, dt);
+    int sp = 0;
+    int cur = R.entry;
+    PTMI_COUNT(0);
+#if PTMI_STATS == 1
+    int n_steps = 0, n_leaves = 0;  // (stats: walks that end at the root / without a leaf)
+#endif
+    while (true) {
+#if PTMI_STATS == 1
+        n_steps++;
+        n_leaves += (cur < 0 && cur != kEmptyChild) ? 1 : 0;
+#endif
+        PTMI_COUNT_ACTIVE(19);  // (stats: wave-level walk loop iterations)
+        PTMI_TSTAMP(t_nd);
+        if (cur >= 0) {
+            int next;
+            const bool down = node_visit(S, stk, cur, sp, rf, ofr, dt, h.t, next);
+            PTMI_TADD(29, t_nd);
+            if (down) {
+                cur = next;
+                continue;
+            }
+        } else if (cur != kEmptyChild) {
+            PTMI_TSTAMP(t_lf);
+            leaf_visit<kVerify>(S, -cur - 1, slot, key, o, d, h, vchain);
+            PTMI_TADD(30, t_lf);
+        }
+        if (sp == 0) break;
+        cur = stk[(--sp) * kStkStride];
+    }
+#if PTMI_STATS == 1
+    if (n_leaves == 0) PTMI_COUNT(20);
+    if (n_steps == 1) PTMI_COUNT(21);
+#endif
 }
 
 // Candidate update as selects (no exec-mask branching).  t > EPSILON implies
@@ -1013,12 +1044,12 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     return h;
 }
 
-// Groups (tracer.cl:598-720), split in two so the walks can be pooled (WalkPool):
-// group_needs_walk is the cheap part -- the conservative cull of each object's
-// traversal hull against the current best -- and walker_loop walks every index that
-// survives, updating the best.  The reference's exact box gates (the object's,
-// tracer.cl:609, and its nodes', 617-719) are checked per winning triangle on its
-// gate chain (chain_certified / verify_chain).
+// Groups (tracer.cl:598-720), split in two so a wave can defer the walks
+// (see trace_groups): group_needs_walk is the cheap part -- the conservative cull
+// of each object's traversal hull against the current best -- and group_walks
+// walks every index that survives, updating h.  The reference's exact box gates
+// (the object's, tracer.cl:609, and its nodes', 617-719) are checked per winning
+// triangle on its gate chain (chain_certified / verify_chain).
 template <bool A>
 __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd, const Hit& h) {
     for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
@@ -1035,6 +1066,67 @@ __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd
         }
     }
     return false;
+}
+
+// The walks of every group object for one ray.  kVerify: eager gate checks on
+// each improving candidate (exact by construction, slower: the check runs
+// inside the divergent walk loop).
+template <bool A, bool kVerify>
+__device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h,
+                                                 bool& cert) {
+    for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
+        const DevObject& ob = S.objs[j];
+        const d4 o = xpt<A>(ob.inv, ob.st, ro);
+        const d4 d = xdir<A>(ob.inv, ob.st, rd);
+        const d4 r = mk(rcp_walk(d.x), rcp_walk(d.y), rcp_walk(d.z), 0.0);
+        PTMI_COUNT(7);
+        // The object's own gate (tracer.cl:609) is the first box of every triangle's
+        // gate chain, so it is checked with the rest of the chain (chain_certified /
+        // verify_chain), not here.
+        int vchain = -1;
+        for (int ci = 0; ci < ob.child_count; ci++) {
+            const RootRec& R = S.root_rec[ob.child_base + ci];
+            double tn;
+            if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
+                         R.hull_mx[2], h.t + prune_margin(h.t), tn))
+                continue;
+            PTMI_TSTAMP(t_w);
+            walk_index<kVerify>(S, stk, R, j, ob.key, o, d, r, h, vchain);
+            PTMI_TADD_ACTIVE(18, t_w);  // (stats: cycles in walk loops)
+        }
+        // Tentative walks: certify the gate chain of a winner from this object while
+        // its object-space ray is at hand (a later object that takes over re-certifies).
+        if (!kVerify && h.tri >= 0 && hit_obj(h) == j) cert = chain_certified(S, S.tris[h.ti].chain, o, d, h.t);
+    }
+}
+
+
+// Deferred gate verification.  The walks first take every Moller-Trumbore hit
+// tentatively; their winner is the minimum over a SUPERSET of the reference's
+// candidates, so if it passes its own gate chain it is the reference's winner.
+// Only then (a lane whose winner fails -- seen only with degenerate boxes, see
+// tests/adversarial.py) are this ray's walks redone with eager checks.  All
+// lanes verify together after the loop instead of one by one inside it.
+template <bool A>
+__device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
+    const Hit h0 = h;
+    bool cert = false;
+    group_walks_impl<A, false>(S, stk, ro, rd, h, cert);
+    if (h.tri >= 0) PTMI_COUNT(4);
+    if (h.tri >= 0 && !cert) {  // the winner is a triangle (h0 holds primitives only) without certificate
+        const DevObject& ob = S.objs[hit_obj(h)];
+        const d4 o = xpt<A>(ob.inv, ob.st, ro);
+        const d4 d = xdir<A>(ob.inv, ob.st, rd);
+        if (!verify_chain(S, S.tris[h.ti].chain, o, d)) {
+            PTMI_COUNT(11);  // (stats build: eager re-walks)
+            h = h0;
+            group_walks_impl<A, true>(S, stk, ro, rd, h, cert);
+        }
+    }
+    if (h.tri >= 0) {  // the winner's barycentrics (for its interpolated normal)
+        const DevObject& ob = S.objs[hit_obj(h)];
+        tri_uv(S.tris[h.ti], xpt<A>(ob.inv, ob.st, ro), xdir<A>(ob.inv, ob.st, rd), h.u, h.v);
+    }
 }
 
 // schlick (tracer.cl:485-505)
@@ -1450,237 +1542,6 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
     return ob.emission[0] > 0.0 || P.b >= kMaxBounces || P.effective >= kMaxEffectiveBounces;
 }
 
-// ---- Group scenes: walker waves serving a workgroup pool of BVH walk requests -------
-//
-// A group-scene workgroup has kTracers tracer waves, which trace paths exactly like the
-// other scenes' waves, and one walker wave, which does every BVH walk of the group.  A
-// tracer lane whose ray needs a walk (group_needs_walk) parks: the ray and its
-// primitives' best (t, pk) go to the lane's slot of the WalkPool (LDS) and the slot's
-// bit is posted; the lane waits while the wave's other lanes go on tracing.  The walker
-// takes posted requests -- a lane whose walk ends takes the next one (refilled in
-// batches of kRefill lanes) -- so its 64 lanes stay busy while requests wait, instead
-// of a wave stopping to walk its own few parked rays for as long as the longest of them
-// takes (round 2: ~27 of 64 lanes walked per walk phase, for a mean walk of 7.9 of the
-// phase's ~28 steps).  The walker writes the result (t, pk, winning triangle) into the
-// slot and sets its done bit; the owner lane picks it up and shades.  Splitting the
-// roles also splits the registers: a tracer carries no walk state and the walker no
-// path state.  Requests are independent and the closest hit is the lexicographic
-// minimum of the same candidates whoever walks, so images are unchanged; each lane
-// still traces its own samples in order.
-static constexpr int kTL = 64 * kTracers;  // tracer lanes = pool slots
-template <bool A>
-struct WalkPool {
-    static constexpr int kC = A ? 3 : 4;  // ray components kept (affine: no w lanes)
-    double ro[kC][kTL], rd[kC][kTL];      // the parked ray, world space
-    double t[kTL];                        // in: the primitives' best t; out: the walks' best
-    int pk[kTL];                          // in / out: its packed object (pack_hit)
-    int ti[kTL];                          // out: the winning triangle's leaf-order index, or -1
-    unsigned long long posted[kTracers];  // bit l of word w: slot 64 w + l waits for the walker
-    unsigned long long done[kTracers];    // bit l of word w: slot 64 w + l has its result
-    int alive;                            // tracer waves still running
-};
-
-#ifndef PTMI_REFILL_WALKERS
-#define PTMI_REFILL_WALKERS 32  // idle lanes that make a walker stop stepping and take more requests
-#endif
-static constexpr int kRefill = PTMI_REFILL_WALKERS;
-
-__device__ __forceinline__ unsigned long long lds_load64(unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ unsigned long long lds_or64(unsigned long long* p, unsigned long long v) {
-    return __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ unsigned long long lds_and64(unsigned long long* p, unsigned long long v) {
-    return __hip_atomic_fetch_and(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// Lanes 0..63 of the wave: popcount of m's bits below this lane.
-__device__ __forceinline__ int rank_below(unsigned long long m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
-
-// Idle walker lanes (req < 0) take posted requests, tracer word `first` first.  Called
-// in wave-uniform control flow with every lane of the wave present.  Per word: the
-// first n set bits of the posted word (n = min(#idle, #posted)) are claimed with one LDS
-// atomic, then the k-th claimed bit goes to the k-th idle lane (two cross-lane
-// permutes); a bit another walker took in between is not received.
-template <bool A>
-__device__ __forceinline__ void claim(WalkPool<A>& Pl, int first, int lane, int& req) {
-    unsigned long long idle = __ballot(req < 0);
-    for (int k = 0; k < kTracers && idle != 0; k++) {
-        const int q = (first + k) % kTracers;
-        const unsigned long long cand = lds_load64(&Pl.posted[q]);
-        if (cand == 0) continue;
-        const int n = min(__popcll(idle), __popcll(cand));
-        const int rb = rank_below(cand);  // rank of bit `lane` among cand's set bits
-        const bool sel = ((cand >> lane) & 1ull) != 0 && rb < n;
-        const unsigned long long want = __ballot(sel);
-        unsigned long long old = 0;
-        if (lane == 0) old = lds_and64(&Pl.posted[q], ~want);
-        const unsigned long long got =
-            kWalkers == 1 ? want
-                          : want & (((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(old >> 32)) << 32) |
-                                    (unsigned)__builtin_amdgcn_readfirstlane((unsigned)old));
-        // Z[r] = the position of the r-th selected bit, held by lane r (push), then the
-        // idle lane of rank r pulls Z[r].  Unselected lanes push to lane 63, which only
-        // matters when n == 64, i.e. when every lane is selected.
-        const int z = __builtin_amdgcn_ds_permute((sel ? rb : 63) * 4, lane);
-        const int ir = rank_below(idle);
-        const int j = __builtin_amdgcn_ds_bpermute(ir * 4, z);
-        if (req < 0 && ir < n && ((got >> j) & 1ull) != 0) req = q * 64 + j;
-        idle = __ballot(req < 0);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// The walker wave (see WalkPool): serve requests until every tracer wave of the group
-// has left.  Per lane the walks of every group object for one request, unrolled into
-// steps so a lane whose walk ends takes the next request: st 1 = set up the walk of
-// group object `obj` (or move on), 2 = one traversal step (a node or a leaf),
-// 3 = verify and publish the result.  The walks take every Moller-Trumbore hit
-// tentatively: their winner is the minimum over a SUPERSET of the reference's
-// candidates, so if it passes its own gate chain it is the reference's winner.  Only
-// when it fails (seen only with degenerate boxes, tests/adversarial.py) is the request
-// walked again `eager`ly, each improving candidate checked against its gate chain as it
-// is found.
-template <int FL>
-__device__ __forceinline__ void walker_loop(const DevScene& S, WalkPool<!(FL & F_PROJ)>& Pl, int* __restrict__ stk,
-                                            int lane) {
-    constexpr bool A = !(FL & F_PROJ);
-    int req = -1, st = 0;
-    int obj = 0, key = 0, cur = 0, sp = 0, vchain = -1;
-    bool cert = false, eager = false;
-    Hit wh{1024.0, -1, -1, -1, 0.0, 0.0};
-    d4 o{}, d{};
-    float rf[3], ofr[3], dt[3];
-    int rot = (threadIdx.x >> 6) % kTracers;  // the tracer word claimed from first (round robin)
-    auto any_posted = [&]() {
-        unsigned long long m = 0;
-        for (int q = 0; q < kTracers; q++) m |= lds_load64(&Pl.posted[q]);
-        return m != 0;
-    };
-    // Publish a finished request: result into the slot, then its done bit.
-    auto publish = [&]() {
-        if (wh.tri >= 0) PTMI_COUNT(4);  // (stats build: certified winners)
-        Pl.t[req] = wh.t;
-        Pl.pk[req] = wh.pk;
-        Pl.ti[req] = wh.tri >= 0 ? wh.ti : -1;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        lds_or64(&Pl.done[req >> 6], 1ull << (req & 63));
-        req = -1;
-        st = 0;
-    };
-    PTMI_TSTAMP(t_wl);
-    for (;;) {
-        PTMI_WADD(23, 1ull);
-        const bool busy = __any(req >= 0);
-        const bool posted = any_posted();
-        if (!busy && !posted) {
-            // A tracer wave leaves only when none of its lanes waits for a walk, so with
-            // every tracer gone no request can appear any more.
-            if (__hip_atomic_load(&Pl.alive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) break;
-            PTMI_TSTAMP(t_sl);
-            __builtin_amdgcn_s_sleep(1);
-            PTMI_WADD(22, 1ull);
-            PTMI_TADD(26, t_sl);
-            continue;
-        }
-        if (posted && __popcll(__ballot(req < 0)) >= (busy ? kRefill : 1)) {
-            const int before = req;
-            claim<A>(Pl, rot, lane, req);
-            rot = rot + 1 == kTracers ? 0 : rot + 1;
-            const bool fresh = req >= 0 && before < 0;
-            PTMI_WADD(24, (unsigned long long)__popcll(__ballot(fresh)));
-            if (fresh) {  // a new request: its primitives' best, the first group object
-                wh = Hit{Pl.t[req], Pl.pk[req], -1, -1, 0.0, 0.0};
-                cert = eager = false;
-                obj = S.run_end[3];
-                st = 1;
-            }
-        }
-        if (st == 1) {  // set up the walk of group object obj (tracer.cl:598-620), or finish
-            if (obj >= S.run_end[4]) {
-                st = 3;
-            } else {
-                const DevObject& ob = S.objs[obj];
-                const d4 wro = mk(Pl.ro[0][req], Pl.ro[1][req], Pl.ro[2][req], A ? 1.0 : Pl.ro[3 % WalkPool<A>::kC][req]);
-                const d4 wrd = mk(Pl.rd[0][req], Pl.rd[1][req], Pl.rd[2][req], A ? 0.0 : Pl.rd[3 % WalkPool<A>::kC][req]);
-                o = xpt<A>(ob.inv, ob.st, wro);
-                d = xdir<A>(ob.inv, ob.st, wrd);
-                const d4 r = mk(rcp_walk(d.x), rcp_walk(d.y), rcp_walk(d.z), 0.0);
-                const RootRec& R = S.root_rec[ob.child_base];  // one traversal index per group object
-                double tn;
-                PTMI_COUNT(7);
-                if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1], R.hull_mx[2],
-                             wh.t + prune_margin(wh.t), tn)) {
-                    obj++;
-                } else {
-                    PTMI_COUNT(0);
-                    walk_setup(o, r, R.bmax, rf, ofr, dt);
-                    key = ob.key;
-                    cur = R.entry;
-                    sp = 0;
-                    vchain = -1;
-                    st = 2;
-                }
-            }
-        }
-        if (st == 3) {  // the deferred gate verification, then publish
-            bool ok = true;
-            if (wh.tri >= 0 && !cert && !eager) {
-                const d4 wro = mk(Pl.ro[0][req], Pl.ro[1][req], Pl.ro[2][req], A ? 1.0 : Pl.ro[3 % WalkPool<A>::kC][req]);
-                const d4 wrd = mk(Pl.rd[0][req], Pl.rd[1][req], Pl.rd[2][req], A ? 0.0 : Pl.rd[3 % WalkPool<A>::kC][req]);
-                const DevObject& ob = S.objs[hit_obj(wh)];
-                ok = verify_chain(S, S.tris[wh.ti].chain, xpt<A>(ob.inv, ob.st, wro), xdir<A>(ob.inv, ob.st, wrd));
-            }
-            if (!ok) {  // walk this request again, eagerly, from its primitives' best
-                PTMI_COUNT(11);  // (stats build: eager re-walks)
-                wh = Hit{Pl.t[req], Pl.pk[req], -1, -1, 0.0, 0.0};
-                eager = true;
-                obj = S.run_end[3];
-                st = 1;
-            } else {
-                publish();
-            }
-        }
-        // Traversal steps of the walking lanes, until enough lanes need a new request
-        // while one is posted, or a lane needs the setup or the verification above.
-        for (;;) {
-            const int n_walk = __popcll(__ballot(st == 2));
-            if (n_walk == 0 || __any(st == 1 || st == 3)) break;
-            if (64 - n_walk >= kRefill && any_posted()) break;
-            PTMI_WADD(19, 1ull);
-            PTMI_WADD(21, (unsigned long long)n_walk);
-            if (st == 2) {  // one step of the walk: a Node4 or a leaf, then pop
-                bool pop = true;
-                if (cur >= 0) {
-                    int next;
-                    if (node_visit(S, stk, cur, sp, rf, ofr, dt, wh.t, next)) {
-                        cur = next;
-                        pop = false;
-                    }
-                } else if (cur != kEmptyChild) {
-                    leaf_visit(S, -cur - 1, obj, key, o, d, wh, vchain, eager);
-                }
-                if (pop) {
-                    if (sp == 0) {  // this object's walk is over: certify a winner from it while its
-                                    // ray is at hand (a later object that takes over re-certifies)
-                        if (!eager && wh.tri >= 0 && hit_obj(wh) == obj)
-                            cert = chain_certified(S, S.tris[wh.ti].chain, o, d, wh.t);
-                        obj++;
-                        if (obj < S.run_end[4]) st = 1;
-                        else if (wh.tri < 0 || cert || eager) publish();  // no verification needed
-                        else st = 3;
-                    } else {
-                        cur = stk[(--sp) * kStkStride];
-                    }
-                }
-            }
-        }
-    }
-    PTMI_TADD(18, t_wl);
-}
-
 // Per-launch resources of trace_kernel<FL>: workgroup size and the register budget.
 #ifndef PTMI_WAVES
 #define PTMI_WAVES 6  // waves/SIMD the register allocation targets (scenes without groups or materials).
@@ -1695,147 +1556,6 @@ __device__ __forceinline__ void walker_loop(const DevScene& S, WalkPool<!(FL & F
 #ifndef PTMI_WAVES_GROUPS
 #define PTMI_WAVES_GROUPS 3  // ... and with BVH groups (the walk needs more registers; 4 spills)
 #endif
-
-// The per-lane sample loop of a tracer wave of a scene with BVH groups (trace_kernel):
-// the loop of the other scenes, with parked lanes waiting for the walker (WalkPool).
-// The pixel's colour sums accumulate in acc_lds.
-template <int FL>
-__device__ __forceinline__ void tracer_loop(const DevScene& S, const double* __restrict__ sunf, WalkPool<!(FL & F_PROJ)>& Pl,
-                                            double* __restrict__ cam_lds, double* __restrict__ acc_lds, int px, int py,
-                                            float fgi, float fgi2, uint64_t seed_bits, uint32_t c0, uint32_t c_end) {
-    constexpr bool A = !(FL & F_PROJ);
-    constexpr bool kDof = (FL & F_DOF) != 0;
-    constexpr int kCamComp = (kDof || !A) ? (A ? 6 : 8) : 3;  // without DoF the origin is the camera's
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    uint32_t n_gen = c0, n_cur = 0;
-    bool buffered = false, active = false, pending = false;
-    PathState P;
-    PTMI_TSTAMP(t_loop);
-    for (;;) {
-        if (!__any(active || buffered || n_gen < c_end)) break;
-        PTMI_TSTAMP(t_a);
-        // Camera rays in wave-wide batches (see trace_kernel).
-        const bool need = !buffered && n_gen < c_end;
-        const int n_need = __popcll(__ballot(need));
-        const int n_starve = __popcll(__ballot(!buffered && !active && n_gen < c_end));
-        if (n_need >= kRefillNeed || n_starve >= PTMI_REFILL_STARVE_GROUPS || (n_starve > 0 && !__any(active))) {
-            if (need) {
-                d4 ro, rd;
-                float rx, ry;
-                camera_offsets<FL>(fgi, fgi2, seed_bits, n_gen, rx, ry);
-                ray_for_pixel<kDof, A>(S.cam, sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n_gen, ro, rd);
-                double* cb = cam_lds + tid;
-                cb[0 * kTL] = rd.x;
-                cb[1 * kTL] = rd.y;
-                cb[2 * kTL] = rd.z;
-                if constexpr (kCamComp > 3) {
-                    cb[3 * kTL] = ro.x;
-                    cb[4 * kTL] = ro.y;
-                    cb[5 * kTL] = ro.z;
-                }
-                if constexpr (!A) {
-                    cb[6 * kTL] = ro.w;
-                    cb[7 * kTL] = rd.w;
-                }
-                n_gen++;
-                buffered = true;
-            }
-        }
-        if (!active && buffered) {
-            const double* cb = cam_lds + tid;
-            const d4 crd = mk(cb[0 * kTL], cb[1 * kTL], cb[2 * kTL], A ? 0.0 : cb[(kCamComp - 1) * kTL]);
-            d4 cro;
-            if constexpr (kCamComp > 3)
-                cro = mk(cb[3 * kTL], cb[4 * kTL], cb[5 * kTL], A ? 1.0 : cb[(kCamComp - 2) * kTL]);
-            else
-                cro = mk(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], 1.0);  // ray_for_pixel's origin
-            start_path<A, kDof>(P, cro, crd);
-            n_cur = n_gen - 1;
-            if constexpr ((FL & F_XRNG) != 0) P.rng = xseed(seed_bits, n_cur);
-            buffered = false;
-            active = true;
-        }
-        PTMI_TADD(12, t_a);
-        // Walk results for this wave's parked lanes; when every active lane is parked and
-        // no result has come, the wave yields its issue slots to the walker for a while.
-        PTMI_TSTAMP(t_c);
-        bool walked = false;
-        const unsigned long long out = __ballot(pending);
-        if (out != 0) {
-            const unsigned long long got = out & lds_load64(&Pl.done[wave]);
-            if (got != 0) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                walked = pending && ((got >> lane) & 1ull) != 0;
-                if (lane == 0) lds_and64(&Pl.done[wave], ~got);
-            } else if (!__any(active && !pending)) {
-                PTMI_WADD(8, 1ull);
-                __builtin_amdgcn_s_sleep(1);
-                PTMI_TADD(14, t_c);
-                continue;
-            }
-        }
-        PTMI_TADD(14, t_c);
-        PTMI_TSTAMP(t_b);
-        bool ready = false;
-        Hit h;
-        if (walked) {  // the walks' closest hit: (t, pk) and the winning triangle's barycentrics
-            pending = false;
-            ready = true;
-            P.ro = mk(Pl.ro[0][tid], Pl.ro[1][tid], Pl.ro[2][tid], A ? 1.0 : Pl.ro[3 % WalkPool<A>::kC][tid]);
-            P.rd = mk(Pl.rd[0][tid], Pl.rd[1][tid], Pl.rd[2][tid], A ? 0.0 : Pl.rd[3 % WalkPool<A>::kC][tid]);
-            h = Hit{Pl.t[tid], Pl.pk[tid], -1, -1, 0.0, 0.0};
-            const int ti = Pl.ti[tid];
-            if (ti >= 0) {
-                const DevTri& T = S.tris[ti];
-                const DevObject& ob = S.objs[hit_obj(h)];
-                h.ti = ti;
-                h.tri = T.n;
-                tri_uv(T, xpt<A>(ob.inv, ob.st, P.ro), xdir<A>(ob.inv, ob.st, P.rd), h.u, h.v);
-            }
-        } else if (active && !pending) {
-            if (P.dead) {
-                h.pk = -1;
-                ready = true;
-            } else {
-                h = find_closest_prims<FL>(S, P.ro, P.rd);
-                if (group_needs_walk<A>(S, P.ro, P.rd, h)) {  // park: post the ray to the pool
-                    pending = true;
-                    Pl.ro[0][tid] = P.ro.x;
-                    Pl.ro[1][tid] = P.ro.y;
-                    Pl.ro[2][tid] = P.ro.z;
-                    Pl.rd[0][tid] = P.rd.x;
-                    Pl.rd[1][tid] = P.rd.y;
-                    Pl.rd[2][tid] = P.rd.z;
-                    if constexpr (!A) {
-                        Pl.ro[3 % WalkPool<A>::kC][tid] = P.ro.w;
-                        Pl.rd[3 % WalkPool<A>::kC][tid] = P.rd.w;
-                    }
-                    Pl.t[tid] = h.t;  // find_closest_prims: tri, ti, u, v are constants
-                    Pl.pk[tid] = h.pk;
-                } else {
-                    ready = true;
-                }
-            }
-        }
-        const unsigned long long posts = __ballot(pending) & ~out;
-        if (posts != 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) lds_or64(&Pl.posted[wave], posts);
-        }
-        PTMI_TADD(13, t_b);
-        PTMI_TSTAMP(t_d);
-        if (ready && bounce_shade<FL>(S, P, h, fgi, n_cur)) {
-            double* a = acc_lds + tid;  // colors += accumColor (tracer.cl:1179), kept in LDS
-            a[0 * kTL] = a[0 * kTL] + P.ar;
-            a[1 * kTL] = a[1 * kTL] + P.ag;
-            a[2 * kTL] = a[2 * kTL] + P.ab;
-            active = false;
-        }
-        PTMI_TADD(15, t_d);
-        PTMI_WADD(10, 1ull);
-    }
-    PTMI_TADD(16, t_loop);
-}
 
 // Work item of a wave (WorkPlan): the tile's pixel of this lane, its sample range and
 // where its sums go.  ok == false: the wave has no item.
@@ -1890,59 +1610,155 @@ __device__ __forceinline__ void store_sums(const Item& it, double* __restrict__ 
     o[3] = (double)(it.c1 > it.c0 ? it.c1 - it.c0 : 0);
 }
 
-// trace_kernel's body for scenes with BVH groups: kTracers tracer waves and one walker
-// wave per workgroup, sharing the walk pool, the walker's traversal stacks and the
-// tracers' camera buffers and colour sums in LDS.
+// trace_kernel's body for scenes with BVH groups: the loop of the other scenes, with
+// the BVH walks deferred.  A lane whose ray needs a walk (group_needs_walk) parks
+// (pending, keeping its primitives' best in LDS) and the wave walks all parked lanes
+// together once kWalkBatch are parked or no lane is ready to shade -- a walk costs the
+// whole wave its longest traversal, so it should run with many lanes, not the ~10 % of
+// rays that reach a mesh in any one bounce.  Each lane still traces its samples in
+// order, and the closest hit does not depend on when or in which order candidates are
+// examined (lexicographic minimum, better()).
 template <int FL>
 __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples, const WorkPlan& WP,
                                              const double* __restrict__ seeds, const double* __restrict__ sunf,
                                              double* __restrict__ sums, double* __restrict__ part) {
     constexpr bool A = !(FL & F_PROJ);
-    constexpr int kCamComp = ((FL & F_DOF) || !A) ? (A ? 6 : 8) : 3;
-    __shared__ WalkPool<A> pool;
-    __shared__ int stk_lds[kWalkers * kStack * kStkStride];
-    __shared__ double acc_lds[3 * kTL];
-    __shared__ double cam_lds[kCamComp * kTL];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    if (tid < kTracers) {  // before any wave can leave
-        pool.posted[tid] = 0;
-        pool.done[tid] = 0;
-    }
-    if (tid == 0) pool.alive = kTracers;
-    __syncthreads();
+    constexpr bool kDof = (FL & F_DOF) != 0;
+    constexpr int kCamComp = (kDof || !A) ? (A ? 6 : 8) : 3;  // see trace_kernel
+    // Per-lane BVH traversal stacks, lane-interleaved (entry k of lane t at
+    // [k * kStkStride + t]) so a wave's pushes and pops hit 64 consecutive dwords; the
+    // per-pixel colour sums (the same additions in the same order) and a parked lane's
+    // primitive best (t, pk), which change once per path or per park, wait in LDS too:
+    // registers are what the walk phases need.
+    __shared__ int stk_lds[kStack * kStkStride];
+    __shared__ double acc_lds[3 * kBlock];
+    __shared__ double hp_t_lds[kBlock];
+    __shared__ int hp_pk_lds[kBlock];
+    __shared__ double cam_lds[kCamComp * kBlock];
+    const int tid = threadIdx.x, lane = tid & 63;
 #if PTMI_STATS
-    if (lane < 32) ptmi_wstat[wave][lane] = 0;
+    if (lane < 32) ptmi_wstat[0][lane] = 0;
 #endif
-    if (wave >= kTracers) {  // a walker
-        walker_loop<FL>(S, pool, stk_lds + (wave - kTracers) * kStack * kStkStride + lane, lane);
-    } else {
-        const Item it = work_item(S, WP, blockIdx.x * kTracers + wave, lane);
-        if (it.ok) {
-            // fgi / fgi2 (tracer.cl:839-841): double division rounded to float.
-            const double seed = it.inside ? seeds[it.i] : 0.0;
-            const float fgi = (float)(seed / (double)S.n_list);
-            const float fgi2 = (float)(seed / (double)samples);
-            acc_lds[0 * kTL + tid] = 0.0;
-            acc_lds[1 * kTL + tid] = 0.0;
-            acc_lds[2 * kTL + tid] = 0.0;
-            tracer_loop<FL>(S, sunf, pool, cam_lds, acc_lds, it.px, it.py, fgi, fgi2,
-                            (uint64_t)__double_as_longlong(seed), it.c0, it.inside ? it.c1 : it.c0);
-            store_sums(it, sums, part, acc_lds[0 * kTL + tid], acc_lds[1 * kTL + tid], acc_lds[2 * kTL + tid]);
+    const Item it = work_item(S, WP, blockIdx.x, lane);
+    if (!it.ok) return;
+    const int px = it.px, py = it.py;
+    // fgi / fgi2 (tracer.cl:839-841): double division rounded to float.
+    const double seed = it.inside ? seeds[it.i] : 0.0;
+    const float fgi = (float)(seed / (double)S.n_list);
+    const float fgi2 = (float)(seed / (double)samples);
+    const uint64_t seed_bits = (uint64_t)__double_as_longlong(seed);
+    const uint32_t c_end = it.inside ? it.c1 : it.c0;
+    int* stk = stk_lds + tid;
+    double* acc = acc_lds + tid;
+    acc[0 * kBlock] = 0.0;
+    acc[1 * kBlock] = 0.0;
+    acc[2 * kBlock] = 0.0;
+    uint32_t n_gen = it.c0, n_cur = 0;
+    bool buffered = false, active = false, pending = false;
+    PathState P;
+    PTMI_TSTAMP(t_loop);
+    for (;;) {
+        if (!__any(active || buffered || n_gen < c_end)) break;
+        PTMI_TSTAMP(t_a);
+        // Camera rays in wave-wide batches (see trace_kernel).
+        const bool need = !buffered && n_gen < c_end;
+        const int n_need = __popcll(__ballot(need));
+        const int n_starve = __popcll(__ballot(!buffered && !active && n_gen < c_end));
+        if (n_need >= kRefillNeed || n_starve >= PTMI_REFILL_STARVE_GROUPS || (n_starve > 0 && !__any(active))) {
+            if (need) {
+                d4 ro, rd;
+                float rx, ry;
+                camera_offsets<FL>(fgi, fgi2, seed_bits, n_gen, rx, ry);
+                ray_for_pixel<kDof, A>(S.cam, sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n_gen, ro, rd);
+                double* cb = cam_lds + tid;
+                cb[0 * kBlock] = rd.x;
+                cb[1 * kBlock] = rd.y;
+                cb[2 * kBlock] = rd.z;
+                if constexpr (kCamComp > 3) {
+                    cb[3 * kBlock] = ro.x;
+                    cb[4 * kBlock] = ro.y;
+                    cb[5 * kBlock] = ro.z;
+                }
+                if constexpr (!A) {
+                    cb[6 * kBlock] = ro.w;
+                    cb[7 * kBlock] = rd.w;
+                }
+                n_gen++;
+                buffered = true;
+            }
         }
-        if (lane == 0) __hip_atomic_fetch_add(&pool.alive, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (!active && buffered) {
+            const double* cb = cam_lds + tid;
+            const d4 crd = mk(cb[0 * kBlock], cb[1 * kBlock], cb[2 * kBlock], A ? 0.0 : cb[(kCamComp - 1) * kBlock]);
+            d4 cro;
+            if constexpr (kCamComp > 3)
+                cro = mk(cb[3 * kBlock], cb[4 * kBlock], cb[5 * kBlock], A ? 1.0 : cb[(kCamComp - 2) * kBlock]);
+            else
+                cro = mk(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], 1.0);  // ray_for_pixel's origin
+            start_path<A, kDof>(P, cro, crd);
+            n_cur = n_gen - 1;
+            if constexpr ((FL & F_XRNG) != 0) P.rng = xseed(seed_bits, n_cur);
+            buffered = false;
+            active = true;
+        }
+        PTMI_TADD(12, t_a);
+        PTMI_TSTAMP(t_b);
+        bool ready = false;
+        Hit h;
+        if (active && !pending) {
+            if (P.dead) {
+                h.pk = -1;
+                ready = true;
+            } else {
+                h = find_closest_prims<FL>(S, P.ro, P.rd);
+                if (group_needs_walk<A>(S, P.ro, P.rd, h)) {
+                    pending = true;
+                    hp_t_lds[tid] = h.t;  // find_closest_prims: tri, ti, u, v are constants
+                    hp_pk_lds[tid] = h.pk;
+                } else {
+                    ready = true;
+                }
+            }
+        }
+        PTMI_TADD(13, t_b);
+        PTMI_TSTAMP(t_c);
+        const int n_pend = __popcll(__ballot(pending));
+        if (n_pend >= kWalkBatch || (n_pend > 0 && !__any(ready))) {
+            PTMI_WADD(8, 1ull);
+            PTMI_WADD(9, (unsigned long long)n_pend);
+            if (pending) {
+                h = Hit{hp_t_lds[tid], hp_pk_lds[tid], -1, -1, 0.0, 0.0};
+                group_walks<A>(S, stk, P.ro, P.rd, h);
+                pending = false;
+                ready = true;
+            }
+        }
+        PTMI_TADD(14, t_c);
+        PTMI_TSTAMP(t_d);
+        if (ready && bounce_shade<FL>(S, P, h, fgi, n_cur)) {
+            acc[0 * kBlock] = acc[0 * kBlock] + P.ar;  // colors += accumColor (tracer.cl:1179)
+            acc[1 * kBlock] = acc[1 * kBlock] + P.ag;
+            acc[2 * kBlock] = acc[2 * kBlock] + P.ab;
+            active = false;
+        }
+        PTMI_TADD(15, t_d);
+        PTMI_WADD(10, 1ull);
     }
+    PTMI_TADD(16, t_loop);
 #if PTMI_STATS
     if (PTMI_FIRST_ACTIVE())
         for (int k = 0; k < 32; k++)
-            if (ptmi_wstat[wave][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[wave][k]);
+            if (ptmi_wstat[0][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[0][k]);
 #endif
+    store_sums(it, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
 }
 
-// Workgroup b runs work items b * w .. b * w + w - 1 of the WorkPlan (w waves per group:
-// Launch<FL>): an 8x8 tile over the whole sample range (sums -> the frame) or a sample
-// chunk of a tail tile (sums -> its slot of the partial buffer).  RGB sums, A = #samples.
+// One wave per workgroup; workgroup b runs work item b of the WorkPlan: an 8x8 tile
+// over the whole sample range (sums -> the frame) or a sample chunk of a tail tile
+// (sums -> its slot of the partial buffer).  A wave that finishes frees its slot (LDS
+// included) at once.  RGB sums, A = #samples.
 template <int FL>
-__global__ __launch_bounds__(Launch<FL>::threads, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
+__global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
                                                   : (FL & F_MATERIALS) ? PTMI_WAVES_MATERIALS
                                                                        : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, WorkPlan WP,
                                                     const double* __restrict__ seeds, const double* __restrict__ sunf,
@@ -2161,8 +1977,8 @@ __global__ __launch_bounds__(256) void seeds_kernel(double* __restrict__ seeds, 
 }
 
 // ---- host-side launch wrappers (called from ptmi_api.cpp) ----------------------
-int trace_block_threads(int flags) { return (flags & F_GROUPS) ? kGB : kBlock; }
-int trace_tiles_per_block(int flags) { return (flags & F_GROUPS) ? kTracers : 1; }  // waves with work items
+int trace_block_threads(int flags) { return kBlock; }
+int trace_tiles_per_block(int flags) { return 1; }
 
 // The instantiation a scene's flags launch: textured and non-affine scenes take the
 // generic ones; F_XRNG exists for the affine instantiations (ptmi_scene_set_rng).
