@@ -1,7 +1,9 @@
-set -e -o pipefail
-OUT=gpurun_out/r3f; mkdir -p $OUT
-timeout -k 10 150 python -u -m pytest tests/test_gpu_parity.py -k "golden or adversarial or live_reference" -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1
-tail -2 $OUT/tests.log
-timeout -k 10 300 python -u -m pytest tests/test_gpu_rng_mode.py tests/test_gpu_go_abi.py -x -q --timeout 200 --timeout-method thread > $OUT/tests2.log 2>&1 || true
-tail -15 $OUT/tests2.log
-bash tools/diag_ab.sh $OUT/ab 512 "c2 c4 c5" "head base"
+set -o pipefail
+OUT=gpurun_out/r3h; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 180 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time --pc-sampling-interval 1 -d $OUT/pcs -o run --output-format csv -- python3 bench.py --config c2 --samples 128 --steps 1 --warmup 0 --no-cpu-baseline --no-trace-call --extra none > $OUT/pcs.log 2>&1
+echo "pcs rc=$?"
+ls -R $OUT/pcs | head -20
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+echo "tests rc=$?"
+tail -5 $OUT/gpu_tests.log
