@@ -1248,7 +1248,7 @@ struct PathState {
     d4 ro, rd;
     double mr, mg, mb;  // mask
     double ar, ag, ab;  // accumColor
-    unsigned b, k, effective;
+    unsigned b, effective;  // bounce index (also the reduction's record index x, tracer.cl:1148-1160), effectiveBounces
     bool inside, done;
     // A camera ray with a NaN component (DoF sample 0: sunflowerRadius(0) =
     // sqrt(-0.5), tracer.cl:224) makes every object-space component NaN in the
@@ -1265,7 +1265,7 @@ __device__ __forceinline__ void start_path(PathState& P, d4 ro, d4 rd) {
     P.rd = rd;
     P.mr = P.mg = P.mb = 1.0;
     P.ar = P.ag = P.ab = 0.0;
-    P.b = P.k = P.effective = 0;
+    P.b = P.effective = 0;
     P.inside = P.done = false;
     P.dead = kDof && !(isfinite(ro.x) && isfinite(ro.y) && isfinite(ro.z) && (A || isfinite(ro.w)) &&
                        isfinite(rd.x) && isfinite(rd.y) && isfinite(rd.z) && (A || isfinite(rd.w)));
@@ -1520,7 +1520,7 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
         P.ag = P.ag + P.mg * eg;
         P.ab = P.ab + P.mb * eb;
         if (er > 0.0) {
-            if (P.k == 0) {
+            if (b == 0) {  // the reduction's first record (tracer.cl:1160): records are per bounce, so x == b
                 P.ar = cr;
                 P.ag = cg;
                 P.ab = cb;
@@ -1536,7 +1536,6 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
         }
     }
     if (!entering && !exiting && !reflecting) P.effective++;
-    P.k++;
     P.b = b + 1;
     // Loop exits of tracer.cl:884 / 1107-1109.
     return ob.emission[0] > 0.0 || P.b >= kMaxBounces || P.effective >= kMaxEffectiveBounces;
@@ -1554,7 +1553,9 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
 #define PTMI_WAVES_MATERIALS 3  // ... with reflective / refractive materials (at 5 they spill 96-112 B/lane)
 #endif
 #ifndef PTMI_WAVES_GROUPS
-#define PTMI_WAVES_GROUPS 3  // ... and with BVH groups (the walk needs more registers; 4 spills)
+#define PTMI_WAVES_GROUPS 4  // ... and with BVH groups: the walk phases need ~155 VGPRs, so 4 waves spill
+                             // 80 B/lane, yet beat 3 waves without spill (512 spp: C4 188 -> 176, C5 294 ->
+                             // 271 ms); round 2, at a demand of ~183 and 128 B/lane of spill, 4 lost 14 %
 #endif
 
 // Work item of a wave (WorkPlan): the tile's pixel of this lane, its sample range and
@@ -1750,7 +1751,9 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
         for (int k = 0; k < 32; k++)
             if (ptmi_wstat[0][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[0][k]);
 #endif
-    store_sums(it, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
+    // The work item is re-derived (a few integer operations) rather than kept live across
+    // the loop: its fields would hold ~5 VGPRs through every walk phase.
+    store_sums(work_item(S, WP, blockIdx.x, lane), sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
 }
 
 // One wave per workgroup; workgroup b runs work item b of the WorkPlan: an 8x8 tile
@@ -1780,7 +1783,14 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
         const float fgi2 = (float)(seed / (double)samples);
         const uint64_t seed_bits = (uint64_t)__double_as_longlong(seed);
         const uint32_t c_end = it.inside ? it.c1 : it.c0;
-        double cr = 0.0, cg = 0.0, cb = 0.0;  // colors (tracer.cl:1179)
+        // colors (tracer.cl:1179): one LDS slot per lane, the same additions in the same
+        // order; they change once per path, and the registers keep the bounce loop off
+        // scratch at the 6-waves/SIMD budget.
+        __shared__ double acc_lds[3 * kBlock];
+        double* acc = acc_lds + tid;
+        acc[0 * kBlock] = 0.0;
+        acc[1 * kBlock] = 0.0;
+        acc[2 * kBlock] = 0.0;
         // Camera rays are produced in wave-wide batches into a one-deep per-lane buffer
         // (LDS) and consumed by path regeneration: generating them at the moment each lane
         // needs one would run the camera block (2 noise3D + the transform) on nearly every
@@ -1851,9 +1861,9 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
             PTMI_TADD(13, t_b);
             PTMI_TSTAMP(t_d);
             if (active && bounce_shade<FL>(S, P, h, fgi, n_cur)) {
-                cr = cr + P.ar;  // colors += accumColor (tracer.cl:1179)
-                cg = cg + P.ag;
-                cb = cb + P.ab;
+                acc[0 * kBlock] = acc[0 * kBlock] + P.ar;  // colors += accumColor (tracer.cl:1179)
+                acc[1 * kBlock] = acc[1 * kBlock] + P.ag;
+                acc[2 * kBlock] = acc[2 * kBlock] + P.ab;
                 active = false;
             }
             PTMI_TADD(15, t_d);
@@ -1865,7 +1875,8 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
             for (int k = 0; k < 32; k++)
                 if (ptmi_wstat[0][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[0][k]);
 #endif
-        store_sums(it, sums, part, cr, cg, cb);
+        store_sums(work_item(S, WP, blockIdx.x, lane), sums, part, acc[0 * kBlock], acc[1 * kBlock],
+                   acc[2 * kBlock]);  // the work item re-derived: fewer live VGPRs
     }
 }
 

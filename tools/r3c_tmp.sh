@@ -1,9 +1,8 @@
-set -o pipefail
-OUT=gpurun_out/r3h; mkdir -p $OUT
-export TMPDIR=/tmp
-timeout -k 10 180 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time --pc-sampling-interval 1 -d $OUT/pcs -o run --output-format csv -- python3 bench.py --config c2 --samples 128 --steps 1 --warmup 0 --no-cpu-baseline --no-trace-call --extra none > $OUT/pcs.log 2>&1
-echo "pcs rc=$?"
-ls -R $OUT/pcs | head -20
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $OUT/gpu_tests.log 2>&1
-echo "tests rc=$?"
-tail -5 $OUT/gpu_tests.log
+#!/bin/bash
+# DIAGNOSTIC scratch: parity subset + A/B timings for the current change
+set -e -o pipefail
+O=gpurun_out/r3c; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_rng_mode.py -x -q --timeout 120 --timeout-method thread > $O/parity.log 2>&1
+tail -2 $O/parity.log
+bash tools/diag_ab.sh $O 512 "c2" "head base w7 w5"
+bash tools/diag_ab.sh $O 512 "c4 c5" "head base"
