@@ -28,6 +28,7 @@ hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, i
 hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint32_t samples, hipStream_t st);
 hipError_t launch_seeds(double* seeds, uint32_t n, uint64_t stream, hipStream_t st);
 hipError_t launch_plane_normals(DevObject* objs, int n, hipStream_t st);
+hipError_t launch_hemi_table(double* out, int* mismatch, hipStream_t st);
 hipError_t launch_combine(const double* parts, uint32_t nparts, size_t npix, double* out, uint32_t samples,
                           hipStream_t st);
 const void* trace_kernel_symbol(int flags);
@@ -40,7 +41,7 @@ using namespace ptmi;
 struct ptmi_scene {
     int device = 0;
     DevScene dev{};
-    void* buffers[13] = {};  // [10..12]: texture arrays
+    void* buffers[14] = {};  // [10..12]: texture arrays, [13]: hemisphere table
     double* partial = nullptr;  // chunk partial sums, grown on demand
     double* sunf = nullptr;     // DoF aperture table for sunf_samples (sunflower_kernel)
     uint32_t sunf_samples = 0;
@@ -456,6 +457,21 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     if (!hs.objs.empty()) {
         SCENE_TRY(launch_plane_normals((DevObject*)s->buffers[0], (int)hs.objs.size(), nullptr));
         SCENE_TRY(hipDeviceSynchronize());
+    }
+    {  // randomVectorInHemisphere table (ptmi_kernels.hip hemi_table_kernel) + its check counter
+        const size_t tab = (size_t)65536 * 4 * sizeof(double);
+        SCENE_TRY(hipMalloc(&s->buffers[13], tab + 256));
+        int* mismatch = (int*)((char*)s->buffers[13] + tab);
+        SCENE_TRY(hipMemset(mismatch, 0, sizeof(int)));
+        SCENE_TRY(launch_hemi_table((double*)s->buffers[13], mismatch, nullptr));
+        int bad = 0;
+        SCENE_TRY(hipMemcpy(&bad, mismatch, sizeof(int), hipMemcpyDeviceToHost));
+        if (bad) {
+            set_err(err, err_len, "hemisphere table: %d records where the affine and generic sequences differ", bad);
+            ptmi_scene_destroy(s);
+            return PTMI_ERR_HIP;
+        }
+        s->dev.hemi = (const double*)s->buffers[13];
     }
     s->dev.roots = (const int32_t*)s->buffers[1];
     s->dev.nodes = (const DevNode*)s->buffers[2];

@@ -151,6 +151,7 @@ struct DevScene {
     uint32_t n_list;  // numObjects of the reference's list (fgi = seed / numObjects, tracer.cl:840)
     DevCamera cam;
     DevTexArray tex[3];  // textures, sphereTextures, cubeMapTextures (tracer.cl:833)
+    const double* hemi;  // randomVectorInHemisphere table, 2^16 x 4 doubles (hemi_table_kernel)
 };
 
 constexpr int kTile = 8;          // a wave64 covers an 8x8 pixel tile

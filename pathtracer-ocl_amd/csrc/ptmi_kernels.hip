@@ -1160,21 +1160,11 @@ __device__ __forceinline__ d4 reflect(d4 rd, d4 nv) { return sub4(rd, scl4(scl4(
 
 // randomVectorInHemisphere (tracer.cl:348-366) from its two uniforms
 // u1 = noise3D(x, y, z), u2 = noise3D(y, z, x) (or the statistical mode's draws).
+// Its transcendental half depends on the uniforms alone: (sin, cos)(2 pi u1) and
+// (sqrt(u2), sqrt(1 - u2)), computed here ...
 template <bool A>
-__device__ __forceinline__ d4 random_hemisphere(d4 nv, float u1, float u2) {
-    double rand1 = 2.0 * kPi * (double)u1;
-    double rand2 = (double)u2;
-    // Affine: sqrt's core; rand2 is 0 or a float >= 2^-149, so in its range (and 1 - rand2
-    // is in (0, 1]), sqrt(+0) = +0 kept by the select.
-    double rand2s = A ? (rand2 == 0.0 ? 0.0 : sqrt_core(rand2)) : sqrt(rand2);
-    // cross(axis, n) for a unit axis: the fma chains of opencl.bc's cross reduce
-    // exactly (up to the sign of exact zeros) to component moves:
-    //   cross((0,1,0,0), n) = (n.z, 0, -n.x, 0),  cross((1,0,0,0), n) = (0, -n.z, n.y, 0)
-    d4 c = fabs(nv.x) > 0.1 ? mk(nv.z, 0.0, -nv.x, 0.0) : mk(0.0, -nv.z, nv.y, 0.0);
-    // |c|^2 >= 0.01 for a unit normal (|n.x| > 0.1 or n.y^2 + n.z^2 >= 0.99): normalize's core
-    d4 u = A ? norm3_core(c) : normv<A>(c);
-    d4 v = cross4(nv, u);
-    double sr, cr;
+__device__ __forceinline__ void hemi_sincos(float u1, double& sr, double& cr) {
+    const double rand1 = 2.0 * kPi * (double)u1;
     if (PTMI_ABLATE & 4) {
         cr = 1.0 - rand1 * 0.1;
         sr = rand1 * 0.15;
@@ -1183,8 +1173,82 @@ __device__ __forceinline__ d4 random_hemisphere(d4 nv, float u1, float u2) {
     } else {
         sincos(rand1, &sr, &cr);  // ocml sincos == (sin, cos) bit-for-bit: one shared reduction
     }
-    const double rc = A ? sqrt_core(1.0 - rand2) : sqrt(1.0 - rand2);
+}
+template <bool A>
+__device__ __forceinline__ void hemi_sqrt(float u2, double& r2s, double& rc) {
+    const double rand2 = (double)u2;
+    // Affine: sqrt's core; rand2 is 0 or a float >= 2^-149, so in its range (and 1 - rand2
+    // is in (0, 1]), sqrt(+0) = +0 kept by the select.
+    r2s = A ? (rand2 == 0.0 ? 0.0 : sqrt_core(rand2)) : sqrt(rand2);
+    rc = A ? sqrt_core(1.0 - rand2) : sqrt(1.0 - rand2);
+}
+
+// ... or read from a table (DevScene::hemi, hemi_table_kernel) for uniforms on the grid
+// k 2^-16.  noise3D's u = fract(v), v = sin(s) * 43758.5453f, is exact in float and a
+// multiple of ulp(v): of 2^-16 or coarser whenever |v| >= 128, i.e. for all but ~0.2 %
+// of the draws (|sin| < 0.0029).  Record k holds the four values computed by the code
+// above from u = k 2^-16, so a lane reads the bits it would compute (the table kernel
+// checks the affine and generic sequences agree on every record).  Off-grid draws,
+// and the statistical mode's 24-bit uniforms, compute.
+#ifndef PTMI_HEMI_TAB_GROUPS
+#define PTMI_HEMI_TAB_GROUPS 0  // mesh scenes compute: the 2 MB table competes with the BVH for the 4 MB
+                                // L2 of an XCD (512 spp: C5 264 vs 268-269 ms with it, C4 170.6 vs 170.2)
+#endif
+static constexpr int kHemiBits = 16;
+static constexpr int kHemiSize = 1 << kHemiBits;
+__device__ __forceinline__ int hemi_slot(float u) {  // table record of u, or -1 off the grid
+    const float t = u * (float)kHemiSize;  // exact (power of two)
+    const int k = (int)t;
+    return (t == (float)k && (unsigned)k < (unsigned)kHemiSize) ? k : -1;
+}
+
+template <bool A, bool kTab>
+__device__ __forceinline__ d4 random_hemisphere(const double* __restrict__ tab, d4 nv, float u1, float u2) {
+    double sr, cr, rand2s, rc;
+    const int k1 = kTab ? hemi_slot(u1) : -1;
+    if (k1 >= 0) {
+        const double2 q = *reinterpret_cast<const double2*>(tab + 4 * k1);
+        sr = q.x;
+        cr = q.y;
+    } else {
+        hemi_sincos<A>(u1, sr, cr);
+    }
+    const int k2 = kTab ? hemi_slot(u2) : -1;
+    if (k2 >= 0) {
+        const double2 q = *reinterpret_cast<const double2*>(tab + 4 * k2 + 2);
+        rand2s = q.x;
+        rc = q.y;
+    } else {
+        hemi_sqrt<A>(u2, rand2s, rc);
+    }
+    // cross(axis, n) for a unit axis: the fma chains of opencl.bc's cross reduce
+    // exactly (up to the sign of exact zeros) to component moves:
+    //   cross((0,1,0,0), n) = (n.z, 0, -n.x, 0),  cross((1,0,0,0), n) = (0, -n.z, n.y, 0)
+    d4 c = fabs(nv.x) > 0.1 ? mk(nv.z, 0.0, -nv.x, 0.0) : mk(0.0, -nv.z, nv.y, 0.0);
+    // |c|^2 >= 0.01 for a unit normal (|n.x| > 0.1 or n.y^2 + n.z^2 >= 0.99): normalize's core
+    d4 u = A ? norm3_core(c) : normv<A>(c);
+    d4 v = cross4(nv, u);
     return add4(add4(scl4(scl4(u, cr), rand2s), scl4(scl4(v, sr), rand2s)), scl4(nv, rc));
+}
+
+// The table: record k = (sin, cos)(2 pi u), sqrt(u), sqrt(1 - u) for u = k 2^-16, from
+// the affine sequences; `mismatch` counts records where the generic (full-operator)
+// sequences give other bits -- the host refuses the scene then (ptmi_api.cpp).
+__global__ __launch_bounds__(256) void hemi_table_kernel(double* __restrict__ out, int* __restrict__ mismatch) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= kHemiSize) return;
+    const float u = (float)k * (1.0f / (float)kHemiSize);
+    double a[4], g[4];
+    hemi_sincos<true>(u, a[0], a[1]);
+    hemi_sqrt<true>(u, a[2], a[3]);
+    hemi_sincos<false>(u, g[0], g[1]);
+    hemi_sqrt<false>(u, g[2], g[3]);
+    bool same = true;
+    for (int i = 0; i < 4; i++) {
+        out[4 * k + i] = a[i];
+        same = same && __double_as_longlong(a[i]) == __double_as_longlong(g[i]);
+    }
+    if (!same) atomicAdd(mismatch, 1);
 }
 
 // sunflower (tracer.cl:221-248), randomize == false.
@@ -1492,7 +1556,7 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
             u1 = noise3d(fgi, (float)b, (float)n);
             u2 = noise3d((float)b, (float)n, fgi);
         }
-        P.rd = random_hemisphere<A>(nv, u1, u2);
+        P.rd = random_hemisphere<A, !kX && (PTMI_HEMI_TAB_GROUPS || !(FL & F_GROUPS))>(S.hemi, nv, u1, u2);
         cosine = dotv<A>(P.rd, nv);
     }
     P.ro = over;
@@ -1908,6 +1972,11 @@ __global__ void plane_normals_kernel(DevObject* objs, int n) {
     objs[j].plane_n[1] = nv.y;
     objs[j].plane_n[2] = nv.z;
     objs[j].plane_n[3] = nv.w;
+}
+
+hipError_t launch_hemi_table(double* out, int* mismatch, hipStream_t st) {
+    hipLaunchKernelGGL(hemi_table_kernel, dim3(kHemiSize / 256), dim3(256), 0, st, out, mismatch);
+    return hipGetLastError();
 }
 
 hipError_t launch_plane_normals(DevObject* objs, int n, hipStream_t st) {
