@@ -1460,8 +1460,11 @@ __device__ __noinline__ d4 plane_normal_map(const DevTexArray T, const DevObject
 // One bounce (tracer.cl:884-1110).  Returns true when the path has ended.
 // One bounce of the path given its closest hit h (tracer.cl:886-1110 after
 // findClosestIntersection).  Returns true when the path has ended.
-template <int FL>
-__device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, const Hit& h, float fgi, uint32_t n) {
+// kAccLds: accumColor lives in LDS at acm[0, kBlock, 2 kBlock] instead of P.ar/ag/ab
+// (the kernels without meshes; it changes only on bounces that see emission).
+template <int FL, bool kAccLds = false>
+__device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, const Hit& h, float fgi, uint32_t n,
+                                             double* acm = nullptr) {
     constexpr bool A = !(FL & F_PROJ);
     constexpr bool kX = (FL & F_XRNG) != 0;
     if (h.pk < 0) return true;  // a miss repeats identically until b == 10 in the reference
@@ -1580,14 +1583,32 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
                 if (ob.tex) textured_color<A>(S.tex[type == 0 ? 0 : type == 1 ? 1 : 2], ob, pos, cr, cg, cb);
             }
         }
-        P.ar = P.ar + P.mr * er;
-        P.ag = P.ag + P.mg * eg;
-        P.ab = P.ab + P.mb * eb;
+        if constexpr (kAccLds) {
+            // accumColor += mask * emission, skipped when every product is +-0: accumColor
+            // starts at +0 and is never -0 before its last write (a sum is -0 only if both
+            // terms are), so adding +-0 would leave it unchanged.  NaN products are added.
+            const double tr = P.mr * er, tg = P.mg * eg, tb = P.mb * eb;
+            if (!(tr == 0.0 && tg == 0.0 && tb == 0.0)) {
+                acm[0 * kBlock] = acm[0 * kBlock] + tr;
+                acm[1 * kBlock] = acm[1 * kBlock] + tg;
+                acm[2 * kBlock] = acm[2 * kBlock] + tb;
+            }
+        } else {
+            P.ar = P.ar + P.mr * er;
+            P.ag = P.ag + P.mg * eg;
+            P.ab = P.ab + P.mb * eb;
+        }
         if (er > 0.0) {
             if (b == 0) {  // the reduction's first record (tracer.cl:1160): records are per bounce, so x == b
-                P.ar = cr;
-                P.ag = cg;
-                P.ab = cb;
+                if constexpr (kAccLds) {
+                    acm[0 * kBlock] = cr;
+                    acm[1 * kBlock] = cg;
+                    acm[2 * kBlock] = cb;
+                } else {
+                    P.ar = cr;
+                    P.ag = cg;
+                    P.ab = cb;
+                }
             }
             P.done = true;
         } else {
@@ -1855,6 +1876,10 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
         acc[0 * kBlock] = 0.0;
         acc[1 * kBlock] = 0.0;
         acc[2 * kBlock] = 0.0;
+        // accumColor of the lane's current path (bounce_shade kAccLds): 6 VGPRs fewer
+        // through the bounce loop.
+        __shared__ double acm_lds[3 * kBlock];
+        double* acm = acm_lds + tid;
         // Camera rays are produced in wave-wide batches into a one-deep per-lane buffer
         // (LDS) and consumed by path regeneration: generating them at the moment each lane
         // needs one would run the camera block (2 noise3D + the transform) on nearly every
@@ -1910,6 +1935,9 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
                 else
                     cro = mk(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], 1.0);  // ray_for_pixel's origin
                 start_path<A, (FL & F_DOF) != 0>(P, cro, crd);
+                acm[0 * kBlock] = 0.0;
+                acm[1 * kBlock] = 0.0;
+                acm[2 * kBlock] = 0.0;
                 n_cur = n_gen - 1;
                 if constexpr ((FL & F_XRNG) != 0) P.rng = xseed(seed_bits, n_cur);
                 buffered = false;
@@ -1924,10 +1952,10 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
             }
             PTMI_TADD(13, t_b);
             PTMI_TSTAMP(t_d);
-            if (active && bounce_shade<FL>(S, P, h, fgi, n_cur)) {
-                acc[0 * kBlock] = acc[0 * kBlock] + P.ar;  // colors += accumColor (tracer.cl:1179)
-                acc[1 * kBlock] = acc[1 * kBlock] + P.ag;
-                acc[2 * kBlock] = acc[2 * kBlock] + P.ab;
+            if (active && bounce_shade<FL, true>(S, P, h, fgi, n_cur, acm)) {
+                acc[0 * kBlock] = acc[0 * kBlock] + acm[0 * kBlock];  // colors += accumColor (tracer.cl:1179)
+                acc[1 * kBlock] = acc[1 * kBlock] + acm[1 * kBlock];
+                acc[2 * kBlock] = acc[2 * kBlock] + acm[2 * kBlock];
                 active = false;
             }
             PTMI_TADD(15, t_d);
