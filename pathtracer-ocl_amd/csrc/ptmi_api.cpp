@@ -48,6 +48,7 @@ struct ptmi_scene {
     size_t partial_bytes = 0;
     int resident_waves = 0;  // device-wide resident waves of trace_kernel
     uint32_t tail_tiles = 0;  // chunked tiles at the end of an automatic launch; 0: default (see render)
+    uint32_t tail_items = 6;  // chunk items per resident wave slot in the tail (scenes without meshes; see render)
     uint32_t width = 0, height = 0;
     int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
     int rng = PTMI_RNG_NOISE3D;  // ptmi_scene_set_rng: PTMI_RNG_XOSHIRO launches the F_XRNG instantiations
@@ -485,6 +486,7 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     s->dev.n_nodes = hs.n_grp;
     s->dev.n_nodes4 = (int32_t)hs.index.nodes.size();
     if (const char* t = getenv("PTMI_TAIL_TILES")) s->tail_tiles = (uint32_t)atoi(t);  // testing: small frames with whole tiles
+    if (const char* t = getenv("PTMI_TAIL_ITEMS")) s->tail_items = (uint32_t)std::max(1, atoi(t));  // tuning
     s->dev.n_tri = hs.n_tri;
     s->dev.cam = hs.cam;
     SCENE_TRY(resident_waves(s));
@@ -577,12 +579,15 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     const uint32_t owned_tiles = (tiles + tile_stride - 1 - tile_offset) / tile_stride;
     // Work items (WorkPlan, ptmi_device.h).  Automatic (chunks == 0), scenes without
     // meshes: whole tiles first, then the last ~0.5 resident waves' worth of tiles
-    // split into sample chunks, so that short items fill the end of the launch (~8 per
+    // split into sample chunks, so that short items fill the end of the launch (~6 per
     // resident wave slot, >= 32 samples each).  A whole-tile item pays its start-up
     // and the spread of its lanes' path lengths once for the whole range, and sums in
     // sample order without a partial buffer.  C2 (2048 spp, 4096 resident waves): 185.3 ms
     // with every tile chunked; 181.6 / 178.2 / 177.5 / 176.8 / 182.5 ms with 9000 / 4096 /
     // 3072 / 2048 / 1024 chunked tail tiles.
+    // Round 3: ~6 items per slot, with the partials as r, g, b planes (24 B per lane and
+    // item): C2 2048 spp 154.0 / 154.5 / 154.9 / 155.3 ms and 0.164 / 0.143 / 0.131 / 0.12 GB
+    // of HBM traffic per launch at 8 / 6 / 5 / 4 items (profiles/r3/tail_items).
     // Mesh scenes chunk every tile (~32 items per slot): a tile's cost there depends on
     // how much mesh it sees, so whole tiles leave a long tail (C4 801 -> 1008 ms).
     // An explicit chunk count splits every tile.
@@ -596,7 +601,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         const bool mesh = (s->flags & 1) != 0;  // F_GROUPS
         if (!mesh || s->tail_tiles)
             n_tail = std::min<uint32_t>(owned_tiles, s->tail_tiles ? s->tail_tiles : (uint32_t)(s->resident_waves / 2));
-        const uint64_t want = (uint64_t)s->resident_waves * (mesh ? 32 : 8);
+        const uint64_t want = (uint64_t)s->resident_waves * (mesh ? 32 : s->tail_items);
         chunks = (uint32_t)std::min<uint64_t>((want + n_tail - 1) / std::max<uint32_t>(n_tail, 1),
                                               std::max<uint32_t>(range / 32, 1));
     }
@@ -630,7 +635,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         }
     }
     if (tile_stride > 1) HIP_TRY(hipMemsetAsync(sums_dev, 0, (size_t)npix * 4 * sizeof(double), st));  // un-owned tiles
-    const size_t need = (size_t)wp.n_tail * 64 * chunks * 4 * sizeof(double);
+    const size_t need = (size_t)wp.n_tail * 64 * chunks * 3 * sizeof(double);  // r, g, b planes
     if (need > s->partial_bytes) {
         if (s->partial) {
             HIP_TRY(hipStreamSynchronize(st));

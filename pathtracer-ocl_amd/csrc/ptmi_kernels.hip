@@ -1686,14 +1686,24 @@ __device__ __forceinline__ Item work_item(const DevScene& S, const WorkPlan& WP,
     return it;
 }
 
-__device__ __forceinline__ void store_sums(const Item& it, double* __restrict__ sums, double* __restrict__ part, double cr,
-                                           double cg, double cb) {
+// A whole-tile item writes its pixel's (r, g, b, samples) into the frame sums; a chunk
+// item its (r, g, b) into plane k of the partial buffer at k * (nchunks * n_tail * 64)
+// + oslot (reduce_chunks_kernel re-derives the sample counts from the plan).
+__device__ __forceinline__ void store_sums(const Item& it, const WorkPlan& WP, double* __restrict__ sums,
+                                           double* __restrict__ part, double cr, double cg, double cb) {
     if (!it.inside) return;
-    double* o = (it.whole ? sums : part) + it.oslot * 4;
-    o[0] = cr;
-    o[1] = cg;
-    o[2] = cb;
-    o[3] = (double)(it.c1 > it.c0 ? it.c1 - it.c0 : 0);
+    if (it.whole) {
+        double* o = sums + it.oslot * 4;
+        o[0] = cr;
+        o[1] = cg;
+        o[2] = cb;
+        o[3] = (double)(it.c1 > it.c0 ? it.c1 - it.c0 : 0);
+    } else {
+        const size_t plane = (size_t)WP.nchunks * WP.n_tail * 64;
+        part[it.oslot] = cr;
+        part[plane + it.oslot] = cg;
+        part[2 * plane + it.oslot] = cb;
+    }
 }
 
 // trace_kernel's body for scenes with BVH groups: the loop of the other scenes, with
@@ -1838,7 +1848,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
 #endif
     // The work item is re-derived (a few integer operations) rather than kept live across
     // the loop: its fields would hold ~5 VGPRs through every walk phase.
-    store_sums(work_item(S, WP, blockIdx.x, lane), sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
+    store_sums(work_item(S, WP, blockIdx.x, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
 }
 
 // One wave per workgroup; workgroup b runs work item b of the WorkPlan: an 8x8 tile
@@ -1967,7 +1977,7 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
             for (int k = 0; k < 32; k++)
                 if (ptmi_wstat[0][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[0][k]);
 #endif
-        store_sums(work_item(S, WP, blockIdx.x, lane), sums, part, acc[0 * kBlock], acc[1 * kBlock],
+        store_sums(work_item(S, WP, blockIdx.x, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock],
                    acc[2 * kBlock]);  // the work item re-derived: fewer live VGPRs
     }
 }
@@ -2024,13 +2034,15 @@ __global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __rest
     const int px = (int)(tile % (uint32_t)tiles_x) * kTile + (int)(lane & 7);
     const int py = (int)(tile / (uint32_t)tiles_x) * kTile + (int)(lane >> 3);
     if (px >= W || py >= H) return;
+    const size_t plane = (size_t)WP.nchunks * WP.n_tail * 64;
     double r = 0.0, g = 0.0, b = 0.0, a = 0.0;
     for (uint32_t c = 0; c < WP.nchunks; c++) {
-        const double* p = part + ((size_t)c * WP.n_tail * 64 + j) * 4;
+        const double* p = part + (size_t)c * WP.n_tail * 64 + j;
         r = r + p[0];
-        g = g + p[1];
-        b = b + p[2];
-        a = a + p[3];
+        g = g + p[plane];
+        b = b + p[2 * plane];
+        const uint32_t c0 = WP.s_begin + c * WP.chunk_len, c1 = min(WP.s_end, c0 + WP.chunk_len);
+        a = a + (double)(c1 > c0 ? c1 - c0 : 0);  // the chunk item's sample count (work_item)
     }
     double* o = sums + ((size_t)py * W + px) * 4;
     o[0] = r;
