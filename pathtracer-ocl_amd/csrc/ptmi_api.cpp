@@ -24,7 +24,8 @@ namespace ptmi {
 hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const double* seeds,
                         const double* sunf, double* sums, double* part, hipStream_t st);
 hipError_t launch_sunflower(double* out, uint32_t samples, hipStream_t st);
-hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, int W, int H, hipStream_t st);
+hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, int W, int H, bool planes,
+                         hipStream_t st);
 hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint32_t samples, hipStream_t st);
 hipError_t launch_seeds(double* seeds, uint32_t n, uint64_t stream, hipStream_t st);
 hipError_t launch_plane_normals(DevObject* objs, int n, hipStream_t st);
@@ -635,7 +636,8 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         }
     }
     if (tile_stride > 1) HIP_TRY(hipMemsetAsync(sums_dev, 0, (size_t)npix * 4 * sizeof(double), st));  // un-owned tiles
-    const size_t need = (size_t)wp.n_tail * 64 * chunks * 3 * sizeof(double);  // r, g, b planes
+    const bool planes = (s->flags & 1) == 0;  // partial layout (ptmi_kernels.hip store_sums): planes without meshes
+    const size_t need = (size_t)wp.n_tail * 64 * chunks * (planes ? 3 : 4) * sizeof(double);
     if (need > s->partial_bytes) {
         if (s->partial) {
             HIP_TRY(hipStreamSynchronize(st));
@@ -653,7 +655,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         HIP_TRY(hipEventRecord(ev1, st));
         s->events.emplace_back(ev0, ev1);
     }
-    HIP_TRY(launch_reduce(s->partial, sums_dev, wp, (int)W, (int)H, st));
+    HIP_TRY(launch_reduce(s->partial, sums_dev, wp, (int)W, (int)H, planes, st));
     return PTMI_OK;
 }
 

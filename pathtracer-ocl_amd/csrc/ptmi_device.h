@@ -160,9 +160,10 @@ constexpr int kTile = 8;          // a wave64 covers an 8x8 pixel tile
 // tile_offset + k * tile_stride, k = 0, 1, ...  The first n_whole of them are one
 // item each over the whole sample range [s_begin, s_end), summed straight into the
 // frame; the last n_tail are split into nchunks sample chunks of chunk_len, one
-// item each, whose r, g, b sums go to three planes of a partial buffer (chunk-major
-// within a plane: chunk c of tail tile tt at [(c * n_tail + tt) * 64 + lane]) that
-// reduce_chunks_kernel adds up in chunk order.  Items are numbered whole tiles first, so the short chunk items
+// item each, whose sums go to a partial buffer (chunk-major: chunk c of tail tile tt,
+// lane l at slot (c * n_tail + tt) * 64 + l of three planes r, g, b, or, in the mesh
+// kernels, as one (r, g, b, samples) record per slot) that reduce_chunks_kernel adds
+// up in chunk order.  Items are numbered whole tiles first, so the short chunk items
 // fill the end of the launch.
 struct WorkPlan {
     uint32_t s_begin, s_end;

@@ -1686,24 +1686,29 @@ __device__ __forceinline__ Item work_item(const DevScene& S, const WorkPlan& WP,
     return it;
 }
 
-// A whole-tile item writes its pixel's (r, g, b, samples) into the frame sums; a chunk
-// item its (r, g, b) into plane k of the partial buffer at k * (nchunks * n_tail * 64)
-// + oslot (reduce_chunks_kernel re-derives the sample counts from the plan).
+// A whole-tile item writes its pixel's (r, g, b, samples) into the frame sums.  A chunk
+// item: kPlanes (scenes without meshes), its r, g, b into plane k of the partial buffer
+// at k * (nchunks * n_tail * 64) + oslot, the sample counts re-derived by
+// reduce_chunks_kernel (24 B per lane and item); else the same (r, g, b, samples) record
+// as a whole tile.  The register allocation of both kernels is sensitive to this
+// epilogue: the plane store costs the mesh kernels 9 more spill reloads in the loop
+// (C4/C5 +2 %), the row layout ([(item * 3 + k) * 64 + lane]) C2 +0.3 %.
+template <bool kPlanes>
 __device__ __forceinline__ void store_sums(const Item& it, const WorkPlan& WP, double* __restrict__ sums,
                                            double* __restrict__ part, double cr, double cg, double cb) {
     if (!it.inside) return;
-    if (it.whole) {
-        double* o = sums + it.oslot * 4;
-        o[0] = cr;
-        o[1] = cg;
-        o[2] = cb;
-        o[3] = (double)(it.c1 > it.c0 ? it.c1 - it.c0 : 0);
-    } else {
+    if (kPlanes && !it.whole) {
         const size_t plane = (size_t)WP.nchunks * WP.n_tail * 64;
         part[it.oslot] = cr;
         part[plane + it.oslot] = cg;
         part[2 * plane + it.oslot] = cb;
+        return;
     }
+    double* o = (it.whole ? sums : part) + it.oslot * 4;
+    o[0] = cr;
+    o[1] = cg;
+    o[2] = cb;
+    o[3] = (double)(it.c1 > it.c0 ? it.c1 - it.c0 : 0);
 }
 
 // trace_kernel's body for scenes with BVH groups: the loop of the other scenes, with
@@ -1848,7 +1853,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
 #endif
     // The work item is re-derived (a few integer operations) rather than kept live across
     // the loop: its fields would hold ~5 VGPRs through every walk phase.
-    store_sums(work_item(S, WP, blockIdx.x, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
+    store_sums<false>(work_item(S, WP, blockIdx.x, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
 }
 
 // One wave per workgroup; workgroup b runs work item b of the WorkPlan: an 8x8 tile
@@ -1977,7 +1982,7 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
             for (int k = 0; k < 32; k++)
                 if (ptmi_wstat[0][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[0][k]);
 #endif
-        store_sums(work_item(S, WP, blockIdx.x, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock],
+        store_sums<true>(work_item(S, WP, blockIdx.x, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock],
                    acc[2 * kBlock]);  // the work item re-derived: fewer live VGPRs
     }
 }
@@ -2025,7 +2030,7 @@ hipError_t launch_plane_normals(DevObject* objs, int n, hipStream_t st) {
 // The tail tiles' chunk partials (WorkPlan) summed in chunk order (deterministic)
 // into the frame; one thread per tail-tile pixel.
 __global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __restrict__ part, double* __restrict__ sums,
-                                                            WorkPlan WP, int W, int H) {
+                                                            WorkPlan WP, int W, int H, bool planes) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= WP.n_tail * 64) return;
     const uint32_t tt = j >> 6, lane = j & 63;
@@ -2034,15 +2039,23 @@ __global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __rest
     const int px = (int)(tile % (uint32_t)tiles_x) * kTile + (int)(lane & 7);
     const int py = (int)(tile / (uint32_t)tiles_x) * kTile + (int)(lane >> 3);
     if (px >= W || py >= H) return;
-    const size_t plane = (size_t)WP.nchunks * WP.n_tail * 64;
     double r = 0.0, g = 0.0, b = 0.0, a = 0.0;
     for (uint32_t c = 0; c < WP.nchunks; c++) {
-        const double* p = part + (size_t)c * WP.n_tail * 64 + j;
-        r = r + p[0];
-        g = g + p[plane];
-        b = b + p[2 * plane];
-        const uint32_t c0 = WP.s_begin + c * WP.chunk_len, c1 = min(WP.s_end, c0 + WP.chunk_len);
-        a = a + (double)(c1 > c0 ? c1 - c0 : 0);  // the chunk item's sample count (work_item)
+        if (planes) {
+            const size_t plane = (size_t)WP.nchunks * WP.n_tail * 64;
+            const double* p = part + (size_t)c * WP.n_tail * 64 + j;  // store_sums' planes
+            r = r + p[0];
+            g = g + p[plane];
+            b = b + p[2 * plane];
+            const uint32_t c0 = WP.s_begin + c * WP.chunk_len, c1 = min(WP.s_end, c0 + WP.chunk_len);
+            a = a + (double)(c1 > c0 ? c1 - c0 : 0);  // the chunk item's sample count (work_item)
+        } else {
+            const double* p = part + ((size_t)c * WP.n_tail * 64 + j) * 4;  // records
+            r = r + p[0];
+            g = g + p[1];
+            b = b + p[2];
+            a = a + p[3];
+        }
     }
     double* o = sums + ((size_t)py * W + px) * 4;
     o[0] = r;
@@ -2142,10 +2155,11 @@ hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const Wo
     return hipGetLastError();
 }
 
-hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, int W, int H, hipStream_t st) {
+hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, int W, int H, bool planes,
+                         hipStream_t st) {
     if (WP.n_tail == 0) return hipSuccess;
     hipLaunchKernelGGL(reduce_chunks_kernel, dim3((WP.n_tail * 64 + 255) / 256), dim3(256), 0, st, part, sums, WP, W,
-                       H);
+                       H, planes);
     return hipGetLastError();
 }
 

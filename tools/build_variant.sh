@@ -7,13 +7,14 @@ NAME=$1; shift
 cd "$(dirname "$0")/../pathtracer-ocl_amd"
 mkdir -p build/exp
 SRC=csrc
-if [ "$NAME" = head ]; then
+REV=${REV:-HEAD}
+if [ "$NAME" = head ] || [ -n "$FROMREV" ]; then
   SRC=$(mktemp -d)/csrc; mkdir -p $SRC
   for f in ptmi_kernels.hip ptmi_api.cpp ptmi_bvh.cpp ptmi_bvh.h ptmi_device.h ptmi_sinf.h ptmi_fp64core.h; do
-    git show HEAD:pathtracer-ocl_amd/csrc/$f > $SRC/$f
+    git show $REV:pathtracer-ocl_amd/csrc/$f > $SRC/$f
   done
   cp -r ../include $(dirname $SRC)/../include 2>/dev/null || true
-  git show HEAD:include/ptmi.h > $(dirname $SRC)/../include/ptmi.h
+  git show $REV:include/ptmi.h > $(dirname $SRC)/../include/ptmi.h
 fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wno-unused-result \
   "$@" -shared -o build/exp/libptmi_$NAME.so $SRC/ptmi_kernels.hip $SRC/ptmi_api.cpp $SRC/ptmi_bvh.cpp
