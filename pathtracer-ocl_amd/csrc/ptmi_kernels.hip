@@ -290,6 +290,20 @@ __device__ __forceinline__ float xnext(Xrng& r) {
     r.s3 = rotl32(r.s3, 11);
     return (float)(res >> 8) * 0x1p-24f;
 }
+// The hemisphere's two draws at 16 bits (k 2^-16): on the grid of the hemisphere table
+// (random_hemisphere), so the statistical mode never evaluates the sincos / sqrt chain
+// there.  A 2^-16 step in u is ~1e-4 rad of direction, far below the Monte-Carlo noise.
+__device__ __forceinline__ float xnext16(Xrng& r) {
+    const uint32_t res = rotl32(r.s1 * 5u, 7) * 9u;
+    const uint32_t t = r.s1 << 9;
+    r.s2 ^= r.s0;
+    r.s3 ^= r.s1;
+    r.s1 ^= r.s2;
+    r.s0 ^= r.s3;
+    r.s2 ^= t;
+    r.s3 = rotl32(r.s3, 11);
+    return (float)(res >> 16) * 0x1p-16f;
+}
 __device__ __forceinline__ Xrng xseed(uint64_t seed_bits, uint32_t n) {
     const uint64_t base = seed_bits ^ (0x9E3779B97F4A7C15ull * ((uint64_t)n + 1));
     const uint64_t a = splitmix64(base + 0x9E3779B97F4A7C15ull), b = splitmix64(base + 0x3C6EF372FE94F82Aull);
@@ -1188,8 +1202,8 @@ __device__ __forceinline__ void hemi_sqrt(float u2, double& r2s, double& rc) {
 // multiple of ulp(v): of 2^-16 or coarser whenever |v| >= 128, i.e. for all but ~0.2 %
 // of the draws (|sin| < 0.0029).  Record k holds the four values computed by the code
 // above from u = k 2^-16, so a lane reads the bits it would compute (the table kernel
-// checks the affine and generic sequences agree on every record).  Off-grid draws,
-// and the statistical mode's 24-bit uniforms, compute.
+// checks the affine and generic sequences agree on every record).  Off-grid draws
+// compute; the statistical mode draws its hemisphere uniforms on the grid (xnext16).
 #ifndef PTMI_HEMI_TAB_GROUPS
 #define PTMI_HEMI_TAB_GROUPS 0  // mesh scenes compute: the 2 MB table competes with the BVH for the 4 MB
                                 // L2 of an XCD (512 spp: C5 264 vs 268-269 ms with it, C4 170.6 vs 170.2)
@@ -1553,13 +1567,13 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
     } else {
         float u1, u2;
         if constexpr (kX) {
-            u1 = xnext(P.rng);
-            u2 = xnext(P.rng);
+            u1 = xnext16(P.rng);
+            u2 = xnext16(P.rng);
         } else {
             u1 = noise3d(fgi, (float)b, (float)n);
             u2 = noise3d((float)b, (float)n, fgi);
         }
-        P.rd = random_hemisphere<A, !kX && (PTMI_HEMI_TAB_GROUPS || !(FL & F_GROUPS))>(S.hemi, nv, u1, u2);
+        P.rd = random_hemisphere<A, PTMI_HEMI_TAB_GROUPS || !(FL & F_GROUPS)>(S.hemi, nv, u1, u2);
         cosine = dotv<A>(P.rd, nv);
     }
     P.ro = over;
