@@ -50,6 +50,7 @@ struct ptmi_scene {
     int resident_waves = 0;  // device-wide resident waves of trace_kernel
     uint32_t tail_tiles = 0;  // chunked tiles at the end of an automatic launch; 0: default (see render)
     uint32_t tail_items = 6;  // chunk items per resident wave slot in the tail (scenes without meshes; see render)
+    uint32_t mesh_items = 32;  // chunk items per resident wave slot, mesh scenes (every tile chunked)
     uint32_t width = 0, height = 0;
     int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
     int rng = PTMI_RNG_NOISE3D;  // ptmi_scene_set_rng: PTMI_RNG_XOSHIRO launches the F_XRNG instantiations
@@ -488,6 +489,7 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     s->dev.n_nodes4 = (int32_t)hs.index.nodes.size();
     if (const char* t = getenv("PTMI_TAIL_TILES")) s->tail_tiles = (uint32_t)atoi(t);  // testing: small frames with whole tiles
     if (const char* t = getenv("PTMI_TAIL_ITEMS")) s->tail_items = (uint32_t)std::max(1, atoi(t));  // tuning
+    if (const char* t = getenv("PTMI_MESH_ITEMS")) s->mesh_items = (uint32_t)std::max(1, atoi(t));  // tuning
     s->dev.n_tri = hs.n_tri;
     s->dev.cam = hs.cam;
     SCENE_TRY(resident_waves(s));
@@ -602,7 +604,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         const bool mesh = (s->flags & 1) != 0;  // F_GROUPS
         if (!mesh || s->tail_tiles)
             n_tail = std::min<uint32_t>(owned_tiles, s->tail_tiles ? s->tail_tiles : (uint32_t)(s->resident_waves / 2));
-        const uint64_t want = (uint64_t)s->resident_waves * (mesh ? 32 : s->tail_items);
+        const uint64_t want = (uint64_t)s->resident_waves * (mesh ? s->mesh_items : s->tail_items);
         chunks = (uint32_t)std::min<uint64_t>((want + n_tail - 1) / std::max<uint32_t>(n_tail, 1),
                                               std::max<uint32_t>(range / 32, 1));
     }

@@ -650,10 +650,10 @@ __device__ __forceinline__ void walk_setup(d4 o, d4 rw, float bmax, float rf[3],
 // One Node4 of a walk: its four children tested against the FP32 slabs, the hit
 // ones ordered near-to-far; the far ones are pushed (farthest first) and the
 // nearest is returned in `next` (false: no child hit, pop the stack).
-__device__ __forceinline__ bool node_visit(const DevScene& S, int* __restrict__ stk, int cur, int& sp,
-                                           const float rf[3], const float ofr[3], const float dt[3], double ht,
-                                           int& next) {
-    PTMI_COUNT(1);
+// The four child slab tests of Node4 `cur`: k[i] = the child's entry distance, or +inf
+// when it is culled; c[i] = its code.
+__device__ __forceinline__ void node_children(const DevScene& S, int cur, const float rf[3], const float ofr[3],
+                                              const float dt[3], double ht, float k[4], int c[4]) {
     // The node's 112 B as seven 16-B global loads issued together (one wait).  (Staging
     // the top levels in LDS made every node fetch a flat load with an aperture select:
     // C4 796 vs 808, C5 1252 vs 1273 ms per 2048-spp frame without it.)
@@ -668,8 +668,6 @@ __device__ __forceinline__ bool node_visit(const DevScene& S, int* __restrict__ 
                        __float_as_int(q[6].w)};
     const double limd = ht + prune_margin(ht);
     const float lim = (float)limd * (1.0f + 0x1p-22f) + 0x1p-100f;  // >= limd
-    float k[4];
-    int c[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         c[i] = ch[i];
@@ -686,6 +684,15 @@ __device__ __forceinline__ bool node_visit(const DevScene& S, int* __restrict__ 
         const float tf = fminf(fminf(fminf(fmaxf(ax, bx) + dt[0], fmaxf(ay, by) + dt[1]), fmaxf(az, bz) + dt[2]), lim);
         k[i] = tn > tf ? __builtin_huge_valf() : tn;
     }
+}
+
+__device__ __forceinline__ bool node_visit(const DevScene& S, int* __restrict__ stk, int cur, int& sp,
+                                           const float rf[3], const float ofr[3], const float dt[3], double ht,
+                                           int& next) {
+    PTMI_COUNT(1);
+    float k[4];
+    int c[4];
+    node_children(S, cur, rf, ofr, dt, ht, k, c);
     // sort (k, c) ascending: 5 compare-exchanges
 #define PTMI_CX(a, b)                                      \
     if (k[b] < k[a]) {                                     \
@@ -1064,6 +1071,9 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
 // walks every index that survives, updating h.  The reference's exact box gates
 // (the object's, tracer.cl:609, and its nodes', 617-719) are checked per winning
 // triangle on its gate chain (chain_certified / verify_chain).
+#ifndef PTMI_ROOT_PRETEST
+#define PTMI_ROOT_PRETEST 0
+#endif
 template <bool A>
 __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd, const Hit& h) {
     for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
@@ -1075,8 +1085,20 @@ __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd
             const RootRec& R = S.root_rec[ob.child_base + ci];
             double tn;
             if (!cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
-                          R.hull_mx[2], h.t + prune_margin(h.t), tn))
+                          R.hull_mx[2], h.t + prune_margin(h.t), tn)) {
+#if PTMI_ROOT_PRETEST
+                // The walk's first step, the entry Node4's child tests, done here: a ray
+                // that misses all four children would walk the root only, so it need not park.
+                if (R.entry < 0) return true;
+                float rf[3], ofr[3], dt[3], k[4];
+                int c[4];
+                walk_setup(o, r, R.bmax, rf, ofr, dt);
+                node_children(S, R.entry, rf, ofr, dt, h.t, k, c);
+                if (fminf(fminf(k[0], k[1]), fminf(k[2], k[3])) < __builtin_huge_valf()) return true;
+#else
                 return true;
+#endif
+            }
         }
     }
     return false;

@@ -1,9 +1,8 @@
 #!/bin/bash
-# DIAGNOSTIC scratch: statistical-mode tests + timing, then the L2/VALU passes
+# DIAGNOSTIC scratch: traversal counters + group-kernel knobs at 4 waves/SIMD
 set -e -o pipefail
-O=gpurun_out/r3o; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_rng_mode.py -x -q --timeout 300 --timeout-method thread > $O/rng.log 2>&1
-tail -2 $O/rng.log
-timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-trace-call --extra none > $O/c2.json 2> $O/c2.err
-python3 -c "import json;d=json.load(open('$O/c2.json'));print('c2', d['ms_per_step'], 'stat', d.get('statistical_rng',{}).get('ms_per_step'))"
-STAGES="l2 valu" bash tools/profile_round3.sh gpurun_out/prof3
+O=gpurun_out/r3q; mkdir -p $O
+PTMI_LIB=pathtracer-ocl_amd/build/libptmi_stats.so timeout -k 10 200 python tools/bvh_stats.py teapot 16 > $O/teapot_stats.txt 2>&1
+PTMI_LIB=pathtracer-ocl_amd/build/libptmi_stats.so timeout -k 10 200 python tools/bvh_stats.py gopher 16 > $O/gopher_stats.txt 2>&1
+grep -h "walks \|node4\|walks_no_leaf\|walks_root_only\|lanes per walk\|tri_tests" $O/teapot_stats.txt $O/gopher_stats.txt
+bash tools/diag_ab.sh $O 512 "c4 c5" "base rpt wb20 wb28 base:PTMI_MESH_ITEMS=16 base:PTMI_MESH_ITEMS=64 base"
