@@ -1071,9 +1071,6 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
 // walks every index that survives, updating h.  The reference's exact box gates
 // (the object's, tracer.cl:609, and its nodes', 617-719) are checked per winning
 // triangle on its gate chain (chain_certified / verify_chain).
-#ifndef PTMI_ROOT_PRETEST
-#define PTMI_ROOT_PRETEST 0
-#endif
 template <bool A>
 __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd, const Hit& h) {
     for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
@@ -1085,20 +1082,8 @@ __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd
             const RootRec& R = S.root_rec[ob.child_base + ci];
             double tn;
             if (!cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
-                          R.hull_mx[2], h.t + prune_margin(h.t), tn)) {
-#if PTMI_ROOT_PRETEST
-                // The walk's first step, the entry Node4's child tests, done here: a ray
-                // that misses all four children would walk the root only, so it need not park.
-                if (R.entry < 0) return true;
-                float rf[3], ofr[3], dt[3], k[4];
-                int c[4];
-                walk_setup(o, r, R.bmax, rf, ofr, dt);
-                node_children(S, R.entry, rf, ofr, dt, h.t, k, c);
-                if (fminf(fminf(k[0], k[1]), fminf(k[2], k[3])) < __builtin_huge_valf()) return true;
-#else
+                          R.hull_mx[2], h.t + prune_margin(h.t), tn))
                 return true;
-#endif
-            }
         }
     }
     return false;
