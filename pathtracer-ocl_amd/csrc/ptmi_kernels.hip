@@ -1656,7 +1656,9 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
                       // 167.9, C3 179.5 -> 174.9 ms); 7 waves (72 VGPRs, 96 B/lane) lose 10 %
 #endif
 #ifndef PTMI_WAVES_MATERIALS
-#define PTMI_WAVES_MATERIALS 3  // ... with reflective / refractive materials (at 5 they spill 96-112 B/lane)
+#define PTMI_WAVES_MATERIALS 5  // ... with reflective / refractive materials: ~95-101 VGPRs since round 3 (LDS colour
+                                // sums and accumColor), 0-32 B/lane of spill at 5; 256 spp: transparency 56.7 -> 53.5,
+                                // reflection 28.0 -> 24.9, default 37.4 -> 35.6 ms against 3 waves (4: within 1 %)
 #endif
 #ifndef PTMI_WAVES_GROUPS
 #define PTMI_WAVES_GROUPS 4  // ... and with BVH groups: the walk phases need ~155 VGPRs, so 4 waves spill

@@ -1,8 +1,12 @@
 #!/bin/bash
-# DIAGNOSTIC scratch: traversal counters + group-kernel knobs at 4 waves/SIMD
+# DIAGNOSTIC scratch: material variants at 5 waves (product) vs 6; parity
 set -e -o pipefail
-O=gpurun_out/r3q; mkdir -p $O
-PTMI_LIB=pathtracer-ocl_amd/build/libptmi_stats.so timeout -k 10 200 python tools/bvh_stats.py teapot 16 > $O/teapot_stats.txt 2>&1
-PTMI_LIB=pathtracer-ocl_amd/build/libptmi_stats.so timeout -k 10 200 python tools/bvh_stats.py gopher 16 > $O/gopher_stats.txt 2>&1
-grep -h "walks \|node4\|walks_no_leaf\|walks_root_only\|lanes per walk\|tri_tests" $O/teapot_stats.txt $O/gopher_stats.txt
-bash tools/diag_ab.sh $O 512 "c4 c5" "base rpt wb20 wb28 base:PTMI_MESH_ITEMS=16 base:PTMI_MESH_ITEMS=64 base"
+O=gpurun_out/r3s; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $O/parity.log 2>&1
+tail -2 $O/parity.log
+for sc in transparency reflection default; do
+  for v in base m6 base; do
+    L=pathtracer-ocl_amd/build/libptmi.so; [ $v != base ] && L=pathtracer-ocl_amd/build/exp/libptmi_$v.so
+    echo -n "$v: "; PTMI_LIB=$L timeout -k 10 120 python tools/scene_time.py $sc 256 2>&1 | grep spp
+  done
+done
