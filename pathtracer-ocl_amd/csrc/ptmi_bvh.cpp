@@ -185,6 +185,37 @@ struct Builder {
 // (count 0 never occurs: leaves hold 1..kLeafMax triangles).
 int32_t leaf_code(int32_t first, int32_t count) { return -((first << 3) | count) - 1; }
 
+// IEEE binary16 for the Node4 bounds.  Finite and infinite patterns are ordered by
+// ord(h) = +-(h & 0x7fff) (sign from bit 15), so directed rounding is a search over
+// that order with the exact decoder.
+constexpr uint16_t kF16Inf = 0x7c00;
+double f16_value(uint16_t h) {
+    const int e = (h >> 10) & 31, f = h & 1023;
+    const double mag = e == 31 ? (f ? NAN : HUGE_VAL) : e == 0 ? std::ldexp(f, -24) : std::ldexp(1024 + f, e - 25);
+    return (h & 0x8000) ? -mag : mag;
+}
+uint16_t f16_of_ord(int o) { return o >= 0 ? (uint16_t)o : (uint16_t)(0x8000 | -o); }
+// The largest binary16 <= v (-infinity below the range).
+uint16_t f16_down(double v) {
+    int lo = -kF16Inf, hi = kF16Inf;  // f16_value(ord lo) <= v holds for every non-NaN v
+    if (f16_value(f16_of_ord(hi)) <= v) return kF16Inf;
+    while (hi - lo > 1) {  // invariant: value(lo) <= v < value(hi)
+        const int mid = lo + (hi - lo) / 2;
+        (f16_value(f16_of_ord(mid)) <= v ? lo : hi) = mid;
+    }
+    return f16_of_ord(lo);
+}
+// The smallest binary16 >= v (+infinity above the range).
+uint16_t f16_up(double v) {
+    int lo = -kF16Inf, hi = kF16Inf;
+    if (f16_value(f16_of_ord(lo)) >= v) return f16_of_ord(lo);
+    while (hi - lo > 1) {  // invariant: value(lo) < v <= value(hi)
+        const int mid = lo + (hi - lo) / 2;
+        (f16_value(f16_of_ord(mid)) >= v ? hi : lo) = mid;
+    }
+    return f16_of_ord(hi);
+}
+
 }  // namespace
 
 int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, const std::vector<int32_t>& tri_off,
@@ -286,14 +317,12 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
     for (const Prim& p : prims)
         for (int k = 0; k < 3; k++) scale = std::max({scale, std::fabs(p.mn[k]), std::fabs(p.mx[k])});
     const double m = 1e-7 * scale + 1e-300;
-    // float box bounds rounded outward (toward -inf / +inf) from the widened doubles
-    auto down = [](double v) {
-        float f = (float)v;
-        return (double)f > v ? std::nextafter(f, -INFINITY) : f;
-    };
-    auto up = [](double v) {
-        float f = (float)v;
-        return (double)f < v ? std::nextafter(f, INFINITY) : f;
+    // Node4 bounds: binary16, rounded outward from the widened doubles (+-infinity
+    // past the binary16 range: still conservative, and exact in the kernel's slab
+    // arithmetic; bmax, its error bound, runs over the finite bounds).
+    auto bound_abs = [](uint16_t h) {
+        const double v = std::fabs(f16_value(h));
+        return std::isfinite(v) ? (float)v : 0.0f;
     };
     float bmax = 0.0f;
     for (int k = 0; k < 3; k++) {
@@ -355,24 +384,20 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
             if (i < nk) {
                 const BNode& c = B.nodes[kids[i]];
                 for (int k = 0; k < 3; k++) {
-                    nd.mn[k][i] = down(c.mn[k] - m);
-                    nd.mx[k][i] = up(c.mx[k] + m);
-                    bmax = std::max({bmax, std::fabs(nd.mn[k][i]), std::fabs(nd.mx[k][i])});
+                    nd.mn[k][i] = f16_down(c.mn[k] - m);
+                    nd.mx[k][i] = f16_up(c.mx[k] + m);
+                    bmax = std::max({bmax, bound_abs(nd.mn[k][i]), bound_abs(nd.mx[k][i])});
                 }
                 nd.child[i] = 0;  // patched after emit (emit may grow out.nodes)
             } else {
-                // an empty slot: a point box at 1e30, culled by the kernel's slab test for
-                // every ray within its pruning limit (ptmi_kernels.hip node_visit)
-                for (int k = 0; k < 3; k++) nd.mn[k][i] = nd.mx[k][i] = 1e30f;
+                // an empty slot: a point box at +infinity, culled by the kernel's slab
+                // test for every ray (ptmi_kernels.hip node_children)
+                for (int k = 0; k < 3; k++) nd.mn[k][i] = nd.mx[k][i] = kF16Inf;
                 nd.child[i] = kEmptyChild;
             }
         }
         for (int i = 0; i < nk; i++) nd.child[i] = emit(kids[i]);
         out.nodes[slot] = nd;
-    }
-    if (!(bmax < 1e30f)) {
-        std::snprintf(err, err_len, "BVH root %d: coordinates too large for the FP32 traversal boxes", root);
-        return PTMI_ERR_UNSUPPORTED;
     }
     rec->bmax = bmax;
     return PTMI_OK;

@@ -78,17 +78,19 @@ struct alignas(16) ChainBox {
     double mn[3], mx[3];
 };
 
-// 4-wide traversal node over one reference root's triangles (ptmi_bvh.cpp).
-// Boxes are float, rounded outward from the (slightly widened) double bounds;
-// the kernel's FP32 slab test widens each interval by its own error bound.
-// child[i] is a Node4 index (>= 0), a leaf code -((first << 3) | count) - 1
-// (triangles [first, first + count) of DevScene::tris), or kEmptyChild.
-struct alignas(16) Node4 {
-    float mn[3][4];  // [axis][child]
-    float mx[3][4];
+// 4-wide traversal node over one reference root's triangles (ptmi_bvh.cpp): one
+// 64-B line.  Box bounds are IEEE binary16 bit patterns rounded outward from the
+// (slightly widened) double bounds, +-infinity past binary16's range; binary16 ->
+// float is exact, so the kernel's FP32 slab test is the one it ran on float boxes,
+// with the same error bound.  child[i] is a Node4 index (>= 0), a leaf code
+// -((first << 3) | count) - 1 (triangles [first, first + count) of DevScene::tris),
+// or kEmptyChild.
+struct alignas(64) Node4 {
+    uint16_t mn[3][4];  // [axis][child], binary16 bits, rounded toward -inf
+    uint16_t mx[3][4];  // toward +inf
     int32_t child[4];
 };
-static_assert(sizeof(Node4) == 112, "Node4 must stay 112 B");
+static_assert(sizeof(Node4) == 64, "Node4 must stay 64 B");
 constexpr int32_t kEmptyChild = INT32_MIN;
 
 // One BVH root of a group object: the widened hull of all its triangles (the
@@ -96,7 +98,7 @@ constexpr int32_t kEmptyChild = INT32_MIN;
 struct alignas(16) RootRec {
     double hull_mn[3], hull_mx[3];
     int32_t entry;
-    float bmax;  // max |coordinate| over the root's Node4 boxes (FP32 slab error bound)
+    float bmax;  // max finite |bound| over the root's decoded Node4 boxes (FP32 slab error bound)
 };
 static_assert(sizeof(RootRec) == 64, "RootRec must stay 64 B");
 
@@ -138,7 +140,7 @@ struct DevScene {
     const PlaneRec* planes;      // all planes
     const SphereRec* spheres;    // scale+translate spheres (the rest: DevObject path)
     int32_t n_spheres_st;
-    int32_t n_nodes4;  // Node4 count (the first min(n, kLdsNodes) are staged in LDS)
+    int32_t n_nodes4;  // Node4 count
     const int32_t* roots;  // concatenated group roots of all type-4 objects
     const RootRec* root_rec;  // per roots[] slot
     const DevNode* nodes;

@@ -654,18 +654,25 @@ __device__ __forceinline__ void walk_setup(d4 o, d4 rw, float bmax, float rf[3],
 // when it is culled; c[i] = its code.
 __device__ __forceinline__ void node_children(const DevScene& S, int cur, const float rf[3], const float ofr[3],
                                               const float dt[3], double ht, float k[4], int c[4]) {
-    // The node's 112 B as seven 16-B global loads issued together (one wait).  (Staging
-    // the top levels in LDS made every node fetch a flat load with an aperture select:
-    // C4 796 vs 808, C5 1252 vs 1273 ms per 2048-spp frame without it.)
-    const float4* src = reinterpret_cast<const float4*>(S.nodes4) + 7 * cur;
-    float4 q[7];
+    // The node's 64 B as four 16-B global loads issued together (one wait).  Bounds are
+    // binary16 (ptmi_device.h), converted exactly to float inside v_fma_mix_f32, so the
+    // slab test is the float-box one; a bound past the binary16 range is +-inf, whose
+    // slab value is +-inf, exact.  (112-B float nodes, seven loads: 1.9 % slower on C5,
+    // 0.6 % on C4 at 512 spp; a scene-wide 2^s scale of the bounds, 2-14 % slower
+    // whichever way it was applied.)
+    const uint4* src = reinterpret_cast<const uint4*>(S.nodes4) + 4 * cur;
+    uint4 q[4];
 #pragma unroll
-    for (int u = 0; u < 7; u++) q[u] = src[u];
-    const float mnx[4] = {q[0].x, q[0].y, q[0].z, q[0].w}, mny[4] = {q[1].x, q[1].y, q[1].z, q[1].w};
-    const float mnz[4] = {q[2].x, q[2].y, q[2].z, q[2].w}, mxx[4] = {q[3].x, q[3].y, q[3].z, q[3].w};
-    const float mxy[4] = {q[4].x, q[4].y, q[4].z, q[4].w}, mxz[4] = {q[5].x, q[5].y, q[5].z, q[5].w};
-    const int ch[4] = {__float_as_int(q[6].x), __float_as_int(q[6].y), __float_as_int(q[6].z),
-                       __float_as_int(q[6].w)};
+    for (int u = 0; u < 4; u++) q[u] = src[u];
+    auto lo = [](uint32_t w) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu)); };
+    auto hi = [](uint32_t w) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16)); };
+    const float mnx[4] = {lo(q[0].x), hi(q[0].x), lo(q[0].y), hi(q[0].y)};
+    const float mny[4] = {lo(q[0].z), hi(q[0].z), lo(q[0].w), hi(q[0].w)};
+    const float mnz[4] = {lo(q[1].x), hi(q[1].x), lo(q[1].y), hi(q[1].y)};
+    const float mxx[4] = {lo(q[1].z), hi(q[1].z), lo(q[1].w), hi(q[1].w)};
+    const float mxy[4] = {lo(q[2].x), hi(q[2].x), lo(q[2].y), hi(q[2].y)};
+    const float mxz[4] = {lo(q[2].z), hi(q[2].z), lo(q[2].w), hi(q[2].w)};
+    const int ch[4] = {(int)q[3].x, (int)q[3].y, (int)q[3].z, (int)q[3].w};
     const double limd = ht + prune_margin(ht);
     const float lim = (float)limd * (1.0f + 0x1p-22f) + 0x1p-100f;  // >= limd
 #pragma unroll
@@ -678,8 +685,8 @@ __device__ __forceinline__ void node_children(const DevScene& S, int cur, const 
         // culls a box that is behind the origin (tf < 0), beyond the best hit
         // (tn > lim) or missed (tn > tf).  NaN bounds (a NaN ray) drop out of the
         // fmaxf / fminf chains: such a child is entered.  Empty slots hold a point box
-        // at 1e30 (ptmi_bvh.cpp) that no ray within the limit reaches; entering one
-        // would be harmless (kEmptyChild is neither node nor leaf).
+        // at +infinity (ptmi_bvh.cpp): both bounds +-inf, so tn > tf or tf < 0; entering
+        // one would be harmless (kEmptyChild is neither node nor leaf).
         const float tn = fmaxf(fmaxf(fmaxf(fminf(ax, bx) - dt[0], fminf(ay, by) - dt[1]), fminf(az, bz) - dt[2]), 0.0f);
         const float tf = fminf(fminf(fminf(fmaxf(ax, bx) + dt[0], fmaxf(ay, by) + dt[1]), fmaxf(az, bz) + dt[2]), lim);
         k[i] = tn > tf ? __builtin_huge_valf() : tn;

@@ -10,7 +10,10 @@ They target the exactness arguments of the BVH path:
   * "stairs" -- axis-aligned faces sharing edges and vertices: rays through
                 shared edges, boxes touching faces exactly;
   * "dupes"  -- every triangle listed twice: exact t ties between different
-                triangle indices (tie-break by index, both gated).
+                triangle indices (tie-break by index, both gated);
+  * "far"    -- "stairs" plus two small grids at x = +-1e5, past binary16's
+                range: the traversal boxes above them carry +-infinity bounds
+                (ptmi_bvh.cpp), which must stay conservative.
 """
 import os
 import tempfile
@@ -32,7 +35,16 @@ def _grid(nx, ny, x0, y0, s, z, faces, verts, flip=False):
 
 def obj_text(kind):
     verts, faces = [], []
-    if kind == "flat":
+    if kind == "far":
+        text, _ = obj_text("stairs")
+        for line in text.splitlines():
+            if line.startswith("v "):
+                verts.append(tuple(float(x) for x in line.split()[1:]))
+            elif line.startswith("f "):
+                faces.append(tuple(int(x) for x in line.split()[1:]))
+        _grid(2, 2, 1.0e5, -1.0, 0.5, 0.0, faces, verts)
+        _grid(2, 2, -1.0e5 - 1.0, -1.0, 0.5, -1.0, faces, verts)
+    elif kind == "flat":
         _grid(24, 24, -6.0, -1.0, 0.5, 0.0, faces, verts)
     elif kind == "stairs":
         for k in range(8):  # step k: top (y = k/2 + 1/2) and riser (z = -k/2) faces, 4x4 quads each

@@ -248,11 +248,12 @@ def test_errors_are_loud():
     assert out.shape == (8 * 8 * 4,)
 
 
-@pytest.mark.parametrize("kind", ["flat", "stairs", "dupes"])
+@pytest.mark.parametrize("kind", ["flat", "stairs", "dupes", "far"])
 @pytest.mark.parametrize("ap", [0.0, 0.15])
 def test_hip_matches_live_reference_adversarial_bvh(kind, ap):
     """Meshes built to break the BVH exactness arguments (tests/adversarial.py):
-    zero-thickness reference boxes, shared edges, exact t ties."""
+    zero-thickness reference boxes, shared edges, exact t ties, traversal bounds past
+    binary16's range."""
     if not pyoracle.ref_available():
         pytest.skip("oracle/_ref not built")
     from tests import adversarial

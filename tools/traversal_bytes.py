@@ -1,7 +1,7 @@
 """Executed traversal work per primary sample of the BVH configs (C4, C5), counted
 by the kernel's own stats build (libptmi_stats.so, PTMI_STATS=1), for bench.py's
 HBM roofline of those configs (bytes per sample).  Bytes per visit
-follow the device layouts (csrc/ptmi_device.h): a Node4 112 B, a DevTri 80 B, a
+follow the device layouts (csrc/ptmi_device.h): a Node4 64 B, a DevTri 80 B, a
 winning triangle's DevTriShade 128 B.
     on the GPU box:  PTMI_LIB=pathtracer-ocl_amd/build/libptmi_stats.so \
                      python tools/traversal_bytes.py run gpurun_out/traversal.json [spp]
@@ -14,7 +14,7 @@ import sys
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "pathtracer-ocl_amd")]
-NODE4_B, TRI_B, SHADE_B = 112, 80, 128
+NODE4_B, TRI_B, SHADE_B = 64, 80, 128
 CONFIGS = {"c4_teapot_1280x960": "teapot", "c5_gopher_1280x960": "gopher"}
 
 
