@@ -10,7 +10,7 @@ SRC=csrc
 REV=${REV:-HEAD}
 if [ "$NAME" = head ] || [ -n "$FROMREV" ]; then
   SRC=$(mktemp -d)/csrc; mkdir -p $SRC
-  for f in ptmi_kernels.hip ptmi_api.cpp ptmi_bvh.cpp ptmi_bvh.h ptmi_device.h ptmi_sinf.h ptmi_fp64core.h; do
+  for f in ptmi_kernels.hip ptmi_api.cpp ptmi_bvh.cpp ptmi_bvh.h ptmi_device.h ptmi_sinf.h ptmi_fp64core.h ptmi_f16.h; do
     git show $REV:pathtracer-ocl_amd/csrc/$f > $SRC/$f
   done
   cp -r ../include $(dirname $SRC)/../include 2>/dev/null || true
