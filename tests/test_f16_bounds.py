@@ -59,6 +59,7 @@ def _samples():
 
 
 def test_outward_rounding_is_tight(lib):
+    np.seterr(over="ignore")  # nextafter from 65504 toward +inf is inf by design
     for v in _samples():
         lo, hi = lib.t_value(lib.t_down(v)), lib.t_value(lib.t_up(v))
         assert lo <= v <= hi, v
