@@ -64,6 +64,19 @@ L2_PEAK_GBS = 34500.0    # MI355X aggregate L2 bandwidth, 8 XCDs x 4 MiB (MI355X
 PMC_FROZEN = os.path.join(ROOT, "profiles", "pmc_measured.json")
 
 
+def build_id():
+    """A short hash of the kernel library's sources (pathtracer-ocl_amd/csrc, include/):
+    frozen PMC counters (profiles/pmc_measured.json) are reported only for the build
+    they were measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in (os.path.join(ROOT, "pathtracer-ocl_amd", "csrc"), os.path.join(ROOT, "include")):
+        for name in sorted(os.listdir(d)):
+            with open(os.path.join(d, name), "rb") as f:
+                h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:12]
+
+
 def _free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -337,11 +350,18 @@ def main():
                 ac = json.load(f)["workloads"][res["alg_key"]]
         except (OSError, KeyError) as e:
             return {"error": "alg counts unavailable: %s" % e}
+        pmc_note = None
         try:
             with open(PMC_FROZEN) as f:
-                pmc = json.load(f)["workloads"].get(res["alg_key"])
+                frozen = json.load(f)
+            pmc = frozen["workloads"].get(res["alg_key"])
+            pmc_spp = int(frozen.get("spp", 2048))
+            if frozen.get("build") != build_id():
+                pmc_note = ("stale: profiles/pmc_measured.json holds counters of build %s, this build is %s; "
+                            "measured levels omitted" % (frozen.get("build"), build_id()))
+                pmc = None
         except (OSError, KeyError, ValueError):
-            pmc = None
+            pmc, pmc_spp = None, 2048
         rate = res["rate"]  # samples/s of the kernel, rank 0
         kms = res["avg_kernel_ms"]
         f64 = ac["fp64_flops_per_sample"]
@@ -352,8 +372,9 @@ def main():
                 "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "fp64_flops_per_sample": round(f64, 1),
                 "flops_basis": "reference-rule algorithmic count (oracle -DPTO_COUNT), not executed"}
         # HBM bytes per launch measured by rocprofv3 PMC passes of this build (FETCH_SIZE x2 +
-        # WRITE_SIZE, gfx950-corrected), scaled to this launch's share of the frame.
-        share = res["samples_per_launch"] / float(res["frame_samples"])
+        # WRITE_SIZE, gfx950-corrected) on full W x H x pmc_spp frames, scaled to this
+        # launch's samples.
+        share = res["samples_per_launch"] / float(res["config"]["width"] * res["config"]["height"] * pmc_spp)
         traffic = None
         hbm = None
         if pmc and pmc.get("hbm_bytes_per_launch"):
@@ -382,10 +403,11 @@ def main():
                 l2["measured"] = {"bytes_per_launch": round(mb), "GBs": round(mb / (kms * 1e-3) / 1e9, 1),
                                   "frac": round(mb / (kms * 1e-3) / 1e9 / L2_PEAK_GBS, 4),
                                   "l2_hit_rate": pmc.get("l2_hit_rate"), "source": pmc.get("source")}
-            roof = {"bound": "valu_issue_latency",
-                    "bound_detail": "VALU issue with idle lanes in the BVH walk phases and the latency of "
-                                    "their dependent node loads; the L2 and HBM levels below are far from "
-                                    "their peaks (the traversal's working set is L2-resident)",
+            roof = {"bound": "l2",
+                    "bound_detail": "achieved / peak / frac are the L2 level of the traversal's bytes "
+                                    "(working set L2-resident).  Neither L2 nor HBM binds: the counters show "
+                                    "VALU issue with idle lanes in the BVH walk phases and the latency of "
+                                    "their dependent node loads (roofline.valu, profiles/<round>/SUMMARY.md)",
                     "achieved": l2["achieved"], "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": l2["frac"],
                     "level": "l2", "l2": l2, "hbm": hbm,
                     "reference_rule": {"bytes_per_sample": round(ac["bytes_per_sample"], 1),
@@ -396,7 +418,9 @@ def main():
                     "fp64_reference_equivalent": fp64}
             if pmc and pmc.get("valu"):
                 roof["valu"] = pmc["valu"]
-        roof.update({"traffic": None if traffic is None else round(traffic),
+        if pmc_note:
+            roof["pmc_status"] = pmc_note
+        roof.update({"build": build_id(), "traffic": None if traffic is None else round(traffic),
                      "traffic_note": "HBM bytes per launch, rocprofv3 PMC passes of this build "
                                      "(profiles/pmc_measured.json <- profiles/<round>/)",
                      "kernel": "trace_kernel (rank 0)", "kernel_ms_avg": round(kms, 3),

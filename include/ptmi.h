@@ -210,6 +210,17 @@ int ptmi_scene_kernel_time(ptmi_scene* s, double* total_ms, uint32_t* launches, 
 /* Build / ABI identification (kernel name, offload arch, flags). */
 const char* ptmi_build_info(void);
 
+/* Diagnostics, host only (no device call): the traversal index ptmi_scene_create would
+ * build for these records (ptmi_bvh.cpp), summarised into out[0..n_out):
+ *   [0] Node4 count  [1] occupied child slots  [2] sum over occupied slots of the
+ *   decoded child box's surface area, in object-space units  [3] infinite bounds among
+ *   them  [4] largest root scale exponent s (bounds stored as (b - ctr) / 2^s)
+ *   [5] roots.  Index quality (box inflation from the binary16 bounds) can be compared
+ *   across translated or scaled copies of one mesh. */
+int ptmi_index_stats(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
+                     const void* groups, uint32_t n_grp, const void* camera, double* out, int n_out,
+                     char* err, size_t err_len);
+
 #ifdef __cplusplus
 }
 #endif

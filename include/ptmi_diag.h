@@ -1,0 +1,31 @@
+/* ptmi_diag.h -- DIAGNOSTIC entry points of libptmi.so (not part of the drop-in
+ * boundary, include/ptmi.h): the standalone BVH walk kernels measured against the mesh
+ * kernels' in-loop walk phases (tools/walk_bench.py). */
+#ifndef PTMI_DIAG_H
+#define PTMI_DIAG_H
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ptmi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Capture builds only (make -C pathtracer-ocl_amd capture -> build/libptmi_capture.so):
+ * the mesh kernels append each walk of their walk phases, up to cap of them, as a
+ * 64-B request (world ray, primitive best t / key) to req_dev and its result (40 B + pad,
+ * ptmi_device.h WalkRes) to res_dev.  Other builds return PTMI_ERR_UNSUPPORTED. */
+int ptmi_diag_capture_setup(void* req_dev, void* res_dev, uint32_t cap, char* err, size_t err_len);
+int ptmi_diag_capture_count(uint32_t* n, char* err, size_t err_len);
+
+/* Walk n requests of scene s with a standalone kernel, results to res_dev; *ms = its
+ * time (HIP events on hip_stream).  mode 0: one request per lane (walk_kernel); mode 1:
+ * persistent waves with per-lane refill from *counter_dev (walk_pool_kernel). */
+int ptmi_diag_walk(ptmi_scene* s, int mode, const void* req_dev, uint32_t n, void* res_dev,
+                   uint32_t* counter_dev, void* hip_stream, float* ms, char* err, size_t err_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PTMI_DIAG_H */

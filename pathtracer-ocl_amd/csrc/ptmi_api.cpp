@@ -17,8 +17,10 @@
 #include <vector>
 
 #include "../../include/ptmi.h"
+#include "../../include/ptmi_diag.h"
 #include "ptmi_bvh.h"
 #include "ptmi_device.h"
+#include "ptmi_f16.h"
 
 namespace ptmi {
 hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const double* seeds,
@@ -53,6 +55,7 @@ struct ptmi_scene {
     uint32_t mesh_items = 32;  // chunk items per resident wave slot, mesh scenes (every tile chunked)
     uint32_t width = 0, height = 0;
     int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
+    int hemi_mismatch = 0;  // hemisphere-table records where affine and generic sequences differ (upload_scene)
     int rng = PTMI_RNG_NOISE3D;  // ptmi_scene_set_rng: PTMI_RNG_XOSHIRO launches the F_XRNG instantiations
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pending (start, stop) pairs
@@ -467,13 +470,14 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
         int* mismatch = (int*)((char*)s->buffers[13] + tab);
         SCENE_TRY(hipMemset(mismatch, 0, sizeof(int)));
         SCENE_TRY(launch_hemi_table((double*)s->buffers[13], mismatch, nullptr));
-        int bad = 0;
-        SCENE_TRY(hipMemcpy(&bad, mismatch, sizeof(int), hipMemcpyDeviceToHost));
-        if (bad) {
-            set_err(err, err_len, "hemisphere table: %d records where the affine and generic sequences differ", bad);
-            ptmi_scene_destroy(s);
-            return PTMI_ERR_HIP;
-        }
+        // Only the affine instantiations read the table (ptmi_kernels.hip bounce_shade), and
+        // its records are the affine sequences' own results, so a record where the generic
+        // (full-operator) sequences give other bits -- a toolchain or ocml change -- affects
+        // no image: it is counted and reported, not a scene failure.
+        SCENE_TRY(hipMemcpy(&s->hemi_mismatch, mismatch, sizeof(int), hipMemcpyDeviceToHost));
+        if (s->hemi_mismatch && getenv("PTMI_VERBOSE"))
+            fprintf(stderr, "ptmi: hemisphere table: %d records where the affine and generic sequences differ "
+                            "(generic instantiations compute, they never read the table)\n", s->hemi_mismatch);
         s->dev.hemi = (const double*)s->buffers[13];
     }
     s->dev.roots = (const int32_t*)s->buffers[1];
@@ -517,6 +521,41 @@ int ptmi_device_name(int device_index, char* buf, size_t len) {
 
 const char* ptmi_build_info(void) {
     return "ptmi abi=1 arch=gfx950 fp=fp64 contract=off kernels=trace_kernel<F>,reduce_chunks_kernel,finalize_kernel";
+}
+
+int ptmi_index_stats(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri, const void* groups,
+                     uint32_t n_grp, const void* camera, double* out, int n_out, char* err, size_t err_len) {
+    if (!out || n_out <= 0) {
+        set_err(err, err_len, "out == NULL");
+        return PTMI_ERR_ARG;
+    }
+    HostScene hs;
+    int rc = prepare_scene(objects, n_obj, triangles, n_tri, groups, n_grp, camera, nullptr, hs, err, err_len);
+    if (rc) return rc;
+    double st[6] = {(double)hs.index.nodes.size(), 0.0, 0.0, 0.0, 0.0, (double)hs.root_rec.size()};
+    for (const RootRec& R : hs.root_rec) {
+        st[4] = std::max(st[4], std::log2((double)R.sc));
+        std::vector<int32_t> todo;
+        if (R.entry >= 0) todo.push_back(R.entry);
+        while (!todo.empty()) {  // the root's Node4s (children >= 0 are Node4 indices)
+            const Node4& nd = hs.index.nodes[todo.back()];
+            todo.pop_back();
+            for (int i = 0; i < 4; i++) {
+                if (nd.child[i] == kEmptyChild) continue;
+                if (nd.child[i] >= 0) todo.push_back(nd.child[i]);
+                double e[3];
+                for (int k = 0; k < 3; k++) {
+                    const double lo = f16_value(nd.bnd[k][0][i]), hi = f16_value(nd.bnd[k][1][i]);
+                    st[3] += (std::isinf(lo) ? 1 : 0) + (std::isinf(hi) ? 1 : 0);
+                    e[k] = (hi - lo) * R.sc;
+                }
+                st[1] += 1.0;
+                st[2] += 2.0 * (e[0] * e[1] + e[1] * e[2] + e[2] * e[0]);
+            }
+        }
+    }
+    for (int i = 0; i < n_out && i < 6; i++) out[i] = st[i];
+    return PTMI_OK;
 }
 
 int ptmi_scene_create(int device_index, const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
@@ -970,3 +1009,70 @@ int stats_read(unsigned long long* out, int reset);
 // DIAGNOSTIC build only: traversal counters (see PTMI_STATS in ptmi_kernels.hip).
 extern "C" int ptmi_stats_read(unsigned long long* out, int reset) { return ptmi::stats_read(out, reset); }
 #endif
+
+// ---- Diagnostics: standalone BVH walks (include/ptmi_diag.h) -------------------------
+namespace ptmi {
+hipError_t launch_walk(const DevScene& S, int flags, int mode, const WalkReq* req, uint32_t n, WalkRes* res,
+                       uint32_t* next, uint32_t grid, hipStream_t st);
+const void* walk_kernel_symbol(int mode);
+hipError_t capture_setup(WalkReq* req, WalkRes* res, uint32_t cap);
+hipError_t capture_count(uint32_t* n);
+}  // namespace ptmi
+
+extern "C" int ptmi_diag_capture_setup(void* req_dev, void* res_dev, uint32_t cap, char* err, size_t err_len) {
+    const hipError_t e = capture_setup((WalkReq*)req_dev, (WalkRes*)res_dev, cap);
+    if (e == hipErrorNotSupported) {
+        set_err(err, err_len, "not a capture build (make -C pathtracer-ocl_amd capture)");
+        return PTMI_ERR_UNSUPPORTED;
+    }
+    HIP_TRY(e);
+    return PTMI_OK;
+}
+
+extern "C" int ptmi_diag_capture_count(uint32_t* n, char* err, size_t err_len) {
+    const hipError_t e = capture_count(n);
+    if (e == hipErrorNotSupported) {
+        set_err(err, err_len, "not a capture build");
+        return PTMI_ERR_UNSUPPORTED;
+    }
+    HIP_TRY(e);
+    return PTMI_OK;
+}
+
+extern "C" int ptmi_diag_walk(ptmi_scene* s, int mode, const void* req_dev, uint32_t n, void* res_dev,
+                              uint32_t* counter_dev, void* hip_stream, float* ms, char* err, size_t err_len) {
+    if (!s || !req_dev || !res_dev || (mode != 0 && mode != 1) || (mode == 1 && !counter_dev)) {
+        set_err(err, err_len, "ptmi_diag_walk: bad arguments");
+        return PTMI_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = (hipStream_t)hip_stream;
+    uint32_t grid = 0;
+    if (mode == 1) {  // persistent: the resident waves of the pool kernel
+        hipDeviceProp_t p;
+        HIP_TRY(hipGetDeviceProperties(&p, s->device));
+        int per_cu = 0;
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, walk_kernel_symbol(1), 64, 0));
+        grid = (uint32_t)std::max(1, per_cu) * (uint32_t)p.multiProcessorCount;
+        HIP_TRY(hipMemsetAsync(counter_dev, 0, sizeof(uint32_t), st));
+    }
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, st));
+    const hipError_t le = launch_walk(s->dev, s->flags, mode, (const WalkReq*)req_dev, n, (WalkRes*)res_dev,
+                                      counter_dev, grid, st);
+    HIP_TRY(hipEventRecord(e1, st));
+    HIP_TRY(hipEventSynchronize(e1));
+    float t = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (le == hipErrorInvalidValue) {
+        set_err(err, err_len, "standalone walks need an affine, untextured mesh scene");
+        return PTMI_ERR_UNSUPPORTED;
+    }
+    HIP_TRY(le);
+    if (ms) *ms = t;
+    return PTMI_OK;
+}

@@ -193,6 +193,7 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
                        const std::vector<int32_t>& tri_cnt, const int32_t* roots, int n_roots, const double* gate_mn,
                        const double* gate_mx, RootIndex& out, RootRec* rec, char* err, size_t err_len) {
     *rec = RootRec{};
+    rec->sc = 1.0f;
     int32_t* entry = &rec->entry;
     const int32_t root = n_roots > 0 ? roots[0] : -1;  // for messages
     // Reference subtrees of the object's roots (children > 0 are present,
@@ -288,18 +289,35 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
     for (const Prim& p : prims)
         for (int k = 0; k < 3; k++) scale = std::max({scale, std::fabs(p.mn[k]), std::fabs(p.mx[k])});
     const double m = 1e-7 * scale + 1e-300;
-    // Node4 bounds: binary16, rounded outward from the widened doubles (+-infinity
-    // past the binary16 range: still conservative, and exact in the kernel's slab
-    // arithmetic; bmax, its error bound, runs over the finite bounds).
-    auto bound_abs = [](uint16_t h) {
-        const double v = std::fabs(f16_value(h));
+    // The root's frame (RootRec): Node4 bounds are stored as (bound - ctr) / 2^s, ctr
+    // the hull centre rounded to float (an exact double, so the kernel's o - ctr is one
+    // double rounding), 2^s the smallest power of two (s in [0, 28]) that brings the
+    // root's extent under 2^15.  A mesh far from the origin keeps binary16's 11
+    // significant bits on its own extent instead of on its distance from the origin,
+    // and one larger than binary16's range keeps finite bounds.  The double subtraction
+    // rounds by <= 2^-52 scale, far inside the widening m.
+    double ext = 0.0;
+    for (int k = 0; k < 3; k++) {
+        const BNode& hb = B.nodes[broot];
+        rec->hull_mn[k] = hb.mn[k] - m;
+        rec->hull_mx[k] = hb.mx[k] + m;
+        const float c = (float)(0.5 * hb.mn[k] + 0.5 * hb.mx[k]);
+        rec->ctr[k] = std::isfinite(c) ? (double)c : 0.0;
+        ext = std::max({ext, std::fabs(rec->hull_mn[k] - rec->ctr[k]), std::fabs(rec->hull_mx[k] - rec->ctr[k])});
+    }
+    int s = 0;
+    while (s < 28 && ext > std::ldexp(32768.0, s)) s++;
+    const double inv_sc = std::ldexp(1.0, -s), sc = std::ldexp(1.0, s);
+    rec->sc = (float)sc;
+    // Node4 bounds: binary16, rounded outward from the widened doubles in the root's
+    // frame (+-infinity past the binary16 range: still conservative, and exact in the
+    // kernel's slab arithmetic; bmax, its error bound, runs over the finite bounds, in
+    // object-space units relative to ctr).
+    auto bound_abs = [sc](uint16_t h) {
+        const double v = std::fabs(f16_value(h)) * sc;
         return std::isfinite(v) ? (float)v : 0.0f;
     };
     float bmax = 0.0f;
-    for (int k = 0; k < 3; k++) {
-        rec->hull_mn[k] = B.nodes[broot].mn[k] - m;
-        rec->hull_mx[k] = B.nodes[broot].mx[k] + m;
-    }
 
     // Triangles in leaf order.
     const int32_t tri_base = (int32_t)out.tris.size();
@@ -355,15 +373,15 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
             if (i < nk) {
                 const BNode& c = B.nodes[kids[i]];
                 for (int k = 0; k < 3; k++) {
-                    nd.mn[k][i] = f16_down(c.mn[k] - m);
-                    nd.mx[k][i] = f16_up(c.mx[k] + m);
-                    bmax = std::max({bmax, bound_abs(nd.mn[k][i]), bound_abs(nd.mx[k][i])});
+                    nd.bnd[k][0][i] = f16_down(((c.mn[k] - m) - rec->ctr[k]) * inv_sc);
+                    nd.bnd[k][1][i] = f16_up(((c.mx[k] + m) - rec->ctr[k]) * inv_sc);
+                    bmax = std::max({bmax, bound_abs(nd.bnd[k][0][i]), bound_abs(nd.bnd[k][1][i])});
                 }
                 nd.child[i] = 0;  // patched after emit (emit may grow out.nodes)
             } else {
                 // an empty slot: a point box at +infinity, culled by the kernel's slab
                 // test for every ray (ptmi_kernels.hip node_children)
-                for (int k = 0; k < 3; k++) nd.mn[k][i] = nd.mx[k][i] = kF16Inf;
+                for (int k = 0; k < 3; k++) nd.bnd[k][0][i] = nd.bnd[k][1][i] = kF16Inf;
                 nd.child[i] = kEmptyChild;
             }
         }

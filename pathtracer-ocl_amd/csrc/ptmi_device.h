@@ -80,27 +80,37 @@ struct alignas(16) ChainBox {
 
 // 4-wide traversal node over one reference root's triangles (ptmi_bvh.cpp): one
 // 64-B line.  Box bounds are IEEE binary16 bit patterns rounded outward from the
-// (slightly widened) double bounds, +-infinity past binary16's range; binary16 ->
-// float is exact, so the kernel's FP32 slab test is the one it ran on float boxes,
-// with the same error bound.  child[i] is a Node4 index (>= 0), a leaf code
+// (slightly widened) double bounds in the root's frame (RootRec), +-infinity past
+// binary16's range; binary16 -> float is exact, so the kernel's FP32 slab test is the
+// one it ran on float boxes, with the same error bound.  Per axis the four children's
+// minima and maxima share one 16-B row, bnd[axis][0 = min, 1 = max][child], so a lane
+// picks its entry and exit planes by the sign of its ray direction with two selects per
+// 8-B half (node_children).  child[i] is a Node4 index (>= 0), a leaf code
 // -((first << 3) | count) - 1 (triangles [first, first + count) of DevScene::tris),
 // or kEmptyChild.
 struct alignas(64) Node4 {
-    uint16_t mn[3][4];  // [axis][child], binary16 bits, rounded toward -inf
-    uint16_t mx[3][4];  // toward +inf
+    uint16_t bnd[3][2][4];  // [axis][min (rounded toward -inf), max (toward +inf)][child]
     int32_t child[4];
 };
 static_assert(sizeof(Node4) == 64, "Node4 must stay 64 B");
 constexpr int32_t kEmptyChild = INT32_MIN;
 
 // One BVH root of a group object: the widened hull of all its triangles (the
-// cull test before its walk) and the entry code of its Node4 index.
+// cull test before its walk) and the entry code of its Node4 index.  The Node4
+// bounds of the root are stored relative to its frame: value = (bound - ctr) / sc,
+// ctr the hull centre rounded to float (an exact double), sc = 2^s (s >= 0) the
+// smallest power of two that brings the root's extent under binary16's range.
+// A mesh far from the origin (an OBJ in millimetres at |x| ~ 1e4) or larger than
+// 65504 units then keeps binary16's 11 significant bits on its own extent.
 struct alignas(16) RootRec {
     double hull_mn[3], hull_mx[3];
+    double ctr[3];
     int32_t entry;
-    float bmax;  // max finite |bound| over the root's decoded Node4 boxes (FP32 slab error bound)
+    float bmax;  // max finite |bound - ctr| over the root's decoded Node4 boxes (FP32 slab error bound)
+    float sc;    // 2^s: the kernel multiplies the ray's FP32 reciprocal by it (walk_setup)
+    int32_t pad;
 };
-static_assert(sizeof(RootRec) == 64, "RootRec must stay 64 B");
+static_assert(sizeof(RootRec) == 96, "RootRec must stay 96 B");
 
 struct alignas(16) DevTriShade {
     double n1[4], n2[4], n3[4];
@@ -155,6 +165,23 @@ struct DevScene {
     DevTexArray tex[3];  // textures, sphereTextures, cubeMapTextures (tracer.cl:833)
     const double* hemi;  // randomVectorInHemisphere table, 2^16 x 4 doubles (hemi_table_kernel)
 };
+
+// One BVH walk of a ray (walk_kernel / walk_pool_kernel): the world-space ray and the
+// best primitive hit so far (t, pk as Hit::pk), one 64-B line; and its result, the
+// closest hit over the primitives and every group object (tri / ti -1 when no triangle
+// wins; u, v the winner's barycentrics).
+struct alignas(16) WalkReq {
+    double o[3], d[3];
+    double t;
+    int32_t pk, pad;
+};
+static_assert(sizeof(WalkReq) == 64, "WalkReq must stay 64 B");
+struct alignas(16) WalkRes {
+    double t;
+    int32_t pk, tri, ti, pad;
+    double u, v;
+};
+static_assert(sizeof(WalkRes) == 40 || sizeof(WalkRes) == 48, "WalkRes size");
 
 constexpr int kTile = 8;          // a wave64 covers an 8x8 pixel tile
 

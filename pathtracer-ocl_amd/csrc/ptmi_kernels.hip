@@ -68,7 +68,21 @@ __shared__ unsigned long long ptmi_wstat[1][32];
 #define PTMI_WADD(i, v) ((void)0)
 #endif
 
+// PTMI_CAPTURE: DIAGNOSTIC build (make capture) -- the mesh kernels record each BVH walk
+// of their walk phases (the ray, the primitive best it starts from, and the result)
+// into device buffers set by ptmi_diag_capture_setup, for the standalone walk kernels'
+// measurement (tools/walk_bench.py).  Same images; the product has PTMI_CAPTURE == 0.
+#ifndef PTMI_CAPTURE
+#define PTMI_CAPTURE 0
+#endif
+
 namespace ptmi {
+
+#if PTMI_CAPTURE
+__device__ WalkReq* ptmi_cap_req;
+__device__ WalkRes* ptmi_cap_res;
+__device__ unsigned ptmi_cap_n, ptmi_cap_max;
+#endif
 
 static constexpr unsigned kMaxEffectiveBounces = 4;  // tracer.cl:2
 static constexpr unsigned kMaxBounces = 10;          // tracer.cl:3
@@ -567,6 +581,11 @@ __device__ __forceinline__ void tri_uv(const DevTri& T, d4 o, d4 d, double& u, d
 }
 
 static constexpr int kStack = 24;  // per-lane LDS traversal stack (3 pushes x BVH4 depth <= 7, ptmi_bvh.cpp)
+// The traversal stack's pointer type: LDS (address space 3), so every push and pop is a
+// ds_write / ds_read whatever the optimiser makes of the pointer (a loop-carried generic
+// pointer had turned the pop into a flat load).
+typedef __attribute__((address_space(3))) int LdsInt;
+__device__ __forceinline__ LdsInt* lds_ptr(int* p) { return (LdsInt*)p; }
 
 // The reference's gate for one triangle: every reference node on the path from
 // the walked root to the triangle's node passes intersectRayWithBox
@@ -622,107 +641,139 @@ __device__ __forceinline__ bool cull_box(d4 o, d4 r, double mnx, double mny, dou
     return tn > tf || tn > lim || tf + prune_margin(tf) < kEps;
 }
 
-// walk_index's FP32 ray setup: with of = (float)o, rf = (float)(1/d) (|rf| clamped to
-// 1e30) and t' = fma(b, rf, -RN(of*rf)), the computed slab bound differs from the exact
-// (b - o)/d by at most 2^-23 |r| (|b| + 2|o|) (FP32 roundings of o, r, the product and
-// the fma); each axis interval is widened by dt = 4x that, so the test only rejects
-// boxes the exact line misses.
-__device__ __forceinline__ void walk_setup(d4 o, d4 rw, float bmax, float rf[3], float ofr[3], float dt[3]) {
+// A walk's FP32 ray, in the root's frame (RootRec: bounds b' = b - ctr stored as
+// b' / sc).  With of = (float)(o - ctr), r = (float)(1/d) (|r| clamped to 1e30) and
+// t' = fma(b' / sc, r * sc, -RN(of * r)) = fma(b', r, -RN(of * r)) (sc a power of two:
+// r * sc is exact), the computed slab bound differs from the exact (b - o)/d = (b' - o')/d
+// by at most e = 2^-23 |r| (|b'| + 2|o'|) (FP32 roundings of o', r, the product and the
+// fma; the double rounding of o - ctr adds 2^-53 |o'|); each axis interval is widened by
+// dt = 4e, so the test only rejects boxes the exact line misses.  The widening is folded
+// into the offsets: entry = fma(near, rf, -(of r + dt)), exit = fma(far, rf, -(of r - dt)),
+// whose extra roundings (of the offset sum, <= 2^-24 |of r + dt|, and of the one fma
+// instead of fma then add) stay below e, inside the 3e of slack.  `neg`: the direction's
+// sign per axis, which picks the entry (near) and exit (far) planes: min and max of the
+// node's bounds for r >= 0, max and min for r < 0.
+struct WalkRay {
+    float rf[3];   // r * sc
+    float olo[3];  // of * r + dt
+    float ohi[3];  // of * r - dt
+    bool neg[3];   // r < 0
+};
+__device__ __forceinline__ WalkRay walk_setup(d4 o, d4 rw, const RootRec& R) {
     const double oo[3] = {o.x, o.y, o.z}, rr[3] = {rw.x, rw.y, rw.z};
     float omax = 0.0f;
+    float r[3], ofr[3];
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-        const float of = (float)oo[a];
-        const float r = (float)rr[a];  // rcp_walk: within 2^-40 of 1/d before the float rounding
-        rf[a] = fminf(fmaxf(r, -1e30f), 1e30f);  // NaN stays NaN
-        ofr[a] = of * rf[a];
+        const float of = (float)(oo[a] - R.ctr[a]);
+        r[a] = fminf(fmaxf((float)rr[a], -1e30f), 1e30f);  // rcp_walk: within 2^-40 of 1/d; NaN stays NaN
+        ofr[a] = of * r[a];
         omax = fmaxf(omax, fabsf(of));
     }
-    const float E = 0x1p-21f * (bmax + 2.0f * omax) + 0x1p-120f;
+    const float E = 0x1p-21f * (R.bmax + 2.0f * omax) + 0x1p-120f;
+    WalkRay W;
 #pragma unroll
-    for (int a = 0; a < 3; a++) dt[a] = E * fabsf(rf[a]);
+    for (int a = 0; a < 3; a++) {
+        const float dt = E * fabsf(r[a]);
+        W.olo[a] = ofr[a] + dt;
+        W.ohi[a] = ofr[a] - dt;
+        W.rf[a] = r[a] * R.sc;  // <= 1e30 * 2^28 < FLT_MAX
+        W.neg[a] = r[a] < 0.0f;  // NaN: false (every slab value is NaN anyway)
+    }
+    return W;
 }
 
-// Closest-hit walk of one root's 4-wide traversal index (ptmi_bvh.cpp): nearest
-// child first, the others pushed far-to-near.  Which triangles are FOUND does
-// not depend on the visiting order or the widened boxes (every triangle that
-// can produce a winning t is reached); ties resolve through better_tri.
-// One Node4 of a walk: its four children tested against the FP32 slabs, the hit
-// ones ordered near-to-far; the far ones are pushed (farthest first) and the
-// nearest is returned in `next` (false: no child hit, pop the stack).
-// The four child slab tests of Node4 `cur`: k[i] = the child's entry distance, or +inf
-// when it is culled; c[i] = its code.
-__device__ __forceinline__ void node_children(const DevScene& S, int cur, const float rf[3], const float ofr[3],
-                                              const float dt[3], double ht, float k[4], int c[4]) {
+// The pruning limit of the FP32 child tests, >= h.t + prune_margin(h.t): it changes only
+// when a leaf improves the best hit, so the walk keeps it in a register.
+__device__ __forceinline__ float walk_limit(double ht) {
+    const double limd = ht + prune_margin(ht);
+    return (float)limd * (1.0f + 0x1p-22f) + 0x1p-100f;
+}
+
+// Child order keys: a child's entry distance tn >= 0 (or +inf when culled) in the high
+// word and its code in the low word of a double.  Float bits of non-negative values are
+// ordered like the values, and 2^20 is added to the high word so the double is always a
+// normal number (no denormal or NaN pattern: the high word stays in [2^20, 0x7f900000]),
+// so v_min_f64 / v_max_f64 order the children by entry distance with one instruction per
+// side of a compare-exchange.  (A -0 from the clamp gives a negative key: it sorts first,
+// and the signed compare below still counts it as entered.)
+static constexpr int32_t kKeyBias = 0x00100000;
+static constexpr int32_t kKeyCulled = 0x7f800000 + kKeyBias;
+__device__ __forceinline__ double child_key(float tn, int code) {
+    const uint32_t hi = (uint32_t)(__float_as_int(tn) + kKeyBias);
+    return __hiloint2double((int)hi, code);
+}
+__device__ __forceinline__ bool key_entered(double k) { return __double2hiint(k) < kKeyCulled; }
+__device__ __forceinline__ int key_code(double k) { return __double2loint(k); }
+
+// The four child slab tests of Node4 `cur` (one walk step): keys of its children.
+__device__ __forceinline__ void node_children(const DevScene& S, int cur, const WalkRay& W, float lim, double k[4]) {
     // The node's 64 B as four 16-B global loads issued together (one wait).  Bounds are
     // binary16 (ptmi_device.h), converted exactly to float inside v_fma_mix_f32, so the
     // slab test is the float-box one; a bound past the binary16 range is +-inf, whose
-    // slab value is +-inf, exact.  (112-B float nodes, seven loads: 1.9 % slower on C5,
-    // 0.6 % on C4 at 512 spp; a scene-wide 2^s scale of the bounds, 2-14 % slower
-    // whichever way it was applied.)
+    // slab value is +-inf, exact.  Row a holds the four minima (.x, .y) and the four
+    // maxima (.z, .w) of axis a; the ray's sign picks entry and exit halves (2 selects
+    // per half and axis), so each child needs one fma per plane and no min / max per axis.
     const uint4* src = reinterpret_cast<const uint4*>(S.nodes4) + 4 * cur;
     uint4 q[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) q[u] = src[u];
-    auto lo = [](uint32_t w) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu)); };
-    auto hi = [](uint32_t w) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16)); };
-    const float mnx[4] = {lo(q[0].x), hi(q[0].x), lo(q[0].y), hi(q[0].y)};
-    const float mny[4] = {lo(q[0].z), hi(q[0].z), lo(q[0].w), hi(q[0].w)};
-    const float mnz[4] = {lo(q[1].x), hi(q[1].x), lo(q[1].y), hi(q[1].y)};
-    const float mxx[4] = {lo(q[1].z), hi(q[1].z), lo(q[1].w), hi(q[1].w)};
-    const float mxy[4] = {lo(q[2].x), hi(q[2].x), lo(q[2].y), hi(q[2].y)};
-    const float mxz[4] = {lo(q[2].z), hi(q[2].z), lo(q[2].w), hi(q[2].w)};
+    uint32_t nr[3][2], fr[3][2];
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        nr[a][0] = W.neg[a] ? q[a].z : q[a].x;
+        nr[a][1] = W.neg[a] ? q[a].w : q[a].y;
+        fr[a][0] = W.neg[a] ? q[a].x : q[a].z;
+        fr[a][1] = W.neg[a] ? q[a].y : q[a].w;
+    }
+    auto h16 = [](uint32_t w, int i) {
+        return (float)__builtin_bit_cast(_Float16, (uint16_t)((i & 1) ? (w >> 16) : (w & 0xffffu)));
+    };
     const int ch[4] = {(int)q[3].x, (int)q[3].y, (int)q[3].z, (int)q[3].w};
-    const double limd = ht + prune_margin(ht);
-    const float lim = (float)limd * (1.0f + 0x1p-22f) + 0x1p-100f;  // >= limd
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        c[i] = ch[i];
-        const float ax = fmaf(mnx[i], rf[0], -ofr[0]), bx = fmaf(mxx[i], rf[0], -ofr[0]);
-        const float ay = fmaf(mny[i], rf[1], -ofr[1]), by = fmaf(mxy[i], rf[1], -ofr[1]);
-        const float az = fmaf(mnz[i], rf[2], -ofr[2]), bz = fmaf(mxz[i], rf[2], -ofr[2]);
-        // Entry clamped at 0 and exit clamped at the pruning limit, so one compare
-        // culls a box that is behind the origin (tf < 0), beyond the best hit
-        // (tn > lim) or missed (tn > tf).  NaN bounds (a NaN ray) drop out of the
-        // fmaxf / fminf chains: such a child is entered.  Empty slots hold a point box
-        // at +infinity (ptmi_bvh.cpp): both bounds +-inf, so tn > tf or tf < 0; entering
-        // one would be harmless (kEmptyChild is neither node nor leaf).
-        const float tn = fmaxf(fmaxf(fmaxf(fminf(ax, bx) - dt[0], fminf(ay, by) - dt[1]), fminf(az, bz) - dt[2]), 0.0f);
-        const float tf = fminf(fminf(fminf(fmaxf(ax, bx) + dt[0], fmaxf(ay, by) + dt[1]), fmaxf(az, bz) + dt[2]), lim);
-        k[i] = tn > tf ? __builtin_huge_valf() : tn;
+        float tn = 0.0f, tf = lim;
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            tn = fmaxf(tn, fmaf(h16(nr[a][i >> 1], i), W.rf[a], -W.olo[a]));
+            tf = fminf(tf, fmaf(h16(fr[a][i >> 1], i), W.rf[a], -W.ohi[a]));
+        }
+        // Entry clamped at 0 and exit clamped at the pruning limit, so one compare culls
+        // a box that is behind the origin (tf < 0), beyond the best hit (tn > lim) or
+        // missed (tn > tf).  NaN slab values (a NaN ray) drop out of the fmaxf / fminf
+        // chains: such a child is entered.  Empty slots hold a point box at +infinity
+        // (ptmi_bvh.cpp): both planes +-inf, so tn > tf or tf < 0; entering one would be
+        // harmless (kEmptyChild is neither node nor leaf).
+        k[i] = child_key(tn > tf ? __builtin_huge_valf() : tn, ch[i]);
     }
 }
 
-__device__ __forceinline__ bool node_visit(const DevScene& S, int* __restrict__ stk, int cur, int& sp,
-                                           const float rf[3], const float ofr[3], const float dt[3], double ht,
-                                           int& next) {
+__device__ __forceinline__ bool node_visit(const DevScene& S, LdsInt* __restrict__ stk, int cur, int& sp,
+                                           const WalkRay& W, float lim, int& next) {
     PTMI_COUNT(1);
-    float k[4];
-    int c[4];
-    node_children(S, cur, rf, ofr, dt, ht, k, c);
-    // sort (k, c) ascending: 5 compare-exchanges
-#define PTMI_CX(a, b)                                      \
-    if (k[b] < k[a]) {                                     \
-        const float tk = k[a];                             \
-        k[a] = k[b];                                       \
-        k[b] = tk;                                         \
-        const int tc = c[a];                               \
-        c[a] = c[b];                                       \
-        c[b] = tc;                                         \
+    double k[4];
+    node_children(S, cur, W, lim, k);
+    // sort the keys ascending: 5 compare-exchanges of one v_min_f64 + one v_max_f64
+#define PTMI_CX(a, b)                        \
+    {                                        \
+        const double lo_ = fmin(k[a], k[b]); \
+        const double hi_ = fmax(k[a], k[b]); \
+        k[a] = lo_;                          \
+        k[b] = hi_;                          \
     }
     PTMI_CX(0, 1) PTMI_CX(2, 3) PTMI_CX(0, 2) PTMI_CX(1, 3) PTMI_CX(1, 2)
 #undef PTMI_CX
     // Unconditional stores above the top, the top advanced by the hit flags (sp <= 21
     // before a node, so the stores stay inside the 24 entries): no exec-mask branches
     // per child (C4 798 -> 778, C5 1250 -> 1216 ms per 2048-spp frame).
-    stk[sp * kStkStride] = c[3];
-    sp += k[3] < __builtin_huge_valf() ? 1 : 0;
-    stk[sp * kStkStride] = c[2];
-    sp += k[2] < __builtin_huge_valf() ? 1 : 0;
-    stk[sp * kStkStride] = c[1];
-    sp += k[1] < __builtin_huge_valf() ? 1 : 0;
-    next = c[0];
-    return k[0] < __builtin_huge_valf();
+    stk[sp * kStkStride] = key_code(k[3]);
+    sp += key_entered(k[3]) ? 1 : 0;
+    stk[sp * kStkStride] = key_code(k[2]);
+    sp += key_entered(k[2]) ? 1 : 0;
+    stk[sp * kStkStride] = key_code(k[1]);
+    sp += key_entered(k[1]) ? 1 : 0;
+    next = key_code(k[0]);
+    return key_entered(k[0]);
 }
 
 // The triangles of one leaf (code = first << 3 | count).
@@ -743,10 +794,10 @@ __device__ __forceinline__ void leaf_visit(const DevScene& S, int code, int slot
 // not depend on the visiting order or the widened boxes (every triangle that
 // can produce a winning t is reached); ties resolve through better_tri.
 template <bool kVerify>
-__device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ stk, const RootRec& R, int slot,
+__device__ __forceinline__ void walk_index(const DevScene& S, LdsInt* __restrict__ stk, const RootRec& R, int slot,
                                            int key, d4 o, d4 d, d4 rw, Hit& h, int& vchain) {
-    float rf[3], ofr[3], dt[3];  // FP32 slab tests (walk_setup)
-    walk_setup(o, rw, R.bmax, rf, ofr, dt);
+    const WalkRay W = walk_setup(o, rw, R);  // FP32 slab tests
+    float lim = walk_limit(h.t);
     int sp = 0;
     int cur = R.entry;
     PTMI_COUNT(0);
@@ -762,7 +813,7 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
         PTMI_TSTAMP(t_nd);
         if (cur >= 0) {
             int next;
-            const bool down = node_visit(S, stk, cur, sp, rf, ofr, dt, h.t, next);
+            const bool down = node_visit(S, stk, cur, sp, W, lim, next);
             PTMI_TADD(29, t_nd);
             if (down) {
                 cur = next;
@@ -771,6 +822,7 @@ __device__ __forceinline__ void walk_index(const DevScene& S, int* __restrict__ 
         } else if (cur != kEmptyChild) {
             PTMI_TSTAMP(t_lf);
             leaf_visit<kVerify>(S, -cur - 1, slot, key, o, d, h, vchain);
+            lim = walk_limit(h.t);
             PTMI_TADD(30, t_lf);
         }
         if (sp == 0) break;
@@ -1100,7 +1152,7 @@ __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd
 // each improving candidate (exact by construction, slower: the check runs
 // inside the divergent walk loop).
 template <bool A, bool kVerify>
-__device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h,
+__device__ __forceinline__ void group_walks_impl(const DevScene& S, LdsInt* __restrict__ stk, d4 ro, d4 rd, Hit& h,
                                                  bool& cert) {
     for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
         const DevObject& ob = S.objs[j];
@@ -1136,7 +1188,7 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, int* __restr
 // tests/adversarial.py) are this ray's walks redone with eager checks.  All
 // lanes verify together after the loop instead of one by one inside it.
 template <bool A>
-__device__ __forceinline__ void group_walks(const DevScene& S, int* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
+__device__ __forceinline__ void group_walks(const DevScene& S, LdsInt* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
     const Hit h0 = h;
     bool cert = false;
     group_walks_impl<A, false>(S, stk, ro, rd, h, cert);
@@ -1587,7 +1639,9 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
             u1 = noise3d(fgi, (float)b, (float)n);
             u2 = noise3d((float)b, (float)n, fgi);
         }
-        P.rd = random_hemisphere<A, PTMI_HEMI_TAB_GROUPS || !(FL & F_GROUPS)>(S.hemi, nv, u1, u2);
+        // Only affine instantiations read the table: its records are the affine sequences'
+        // results, so they equal what such a lane computes by construction.
+        P.rd = random_hemisphere<A, A && (PTMI_HEMI_TAB_GROUPS || !(FL & F_GROUPS))>(S.hemi, nv, u1, u2);
         cosine = dotv<A>(P.rd, nv);
     }
     P.ro = over;
@@ -1779,7 +1833,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
     const float fgi2 = (float)(seed / (double)samples);
     const uint64_t seed_bits = (uint64_t)__double_as_longlong(seed);
     const uint32_t c_end = it.inside ? it.c1 : it.c0;
-    int* stk = stk_lds + tid;
+    LdsInt* stk = lds_ptr(stk_lds + tid);
     double* acc = acc_lds + tid;
     acc[0 * kBlock] = 0.0;
     acc[1 * kBlock] = 0.0;
@@ -1842,7 +1896,10 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
                 ready = true;
             } else {
                 h = find_closest_prims<FL>(S, P.ro, P.rd);
-                if (group_needs_walk<A>(S, P.ro, P.rd, h)) {
+                const bool nw = group_needs_walk<A>(S, P.ro, P.rd, h);
+                if (PTMI_ABLATE & 1024) asm volatile("" ::"v"(nw ? 1 : 0));  // DIAGNOSTIC 1024: hull culls kept,
+                                                                              // no walks (the mesh is invisible)
+                if (!(PTMI_ABLATE & 1024) && nw) {
                     pending = true;
                     hp_t_lds[tid] = h.t;  // find_closest_prims: tri, ti, u, v are constants
                     hp_pk_lds[tid] = h.pk;
@@ -1859,7 +1916,15 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
             PTMI_WADD(9, (unsigned long long)n_pend);
             if (pending) {
                 h = Hit{hp_t_lds[tid], hp_pk_lds[tid], -1, -1, 0.0, 0.0};
+#if PTMI_CAPTURE
+                const unsigned ci = atomicAdd(&ptmi_cap_n, 1u);
+                if (ci < ptmi_cap_max)
+                    ptmi_cap_req[ci] = WalkReq{{P.ro.x, P.ro.y, P.ro.z}, {P.rd.x, P.rd.y, P.rd.z}, h.t, h.pk, 0};
+#endif
                 group_walks<A>(S, stk, P.ro, P.rd, h);
+#if PTMI_CAPTURE
+                if (ci < ptmi_cap_max) ptmi_cap_res[ci] = WalkRes{h.t, h.pk, h.tri, h.ti, 0, h.u, h.v};
+#endif
                 pending = false;
                 ready = true;
             }
@@ -2016,6 +2081,175 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
                    acc[2 * kBlock]);  // the work item re-derived: fewer live VGPRs
     }
 }
+
+// ---- Standalone BVH walks (round 4) -------------------------------------------------
+// The mesh kernels walk inside their bounce loop, with the whole path state live: 4
+// waves/SIMD, and a walk phase runs ~24 parked lanes of 64 for as long as the longest
+// walk.  These kernels walk a list of requests (WalkReq: world ray + primitive best) with
+// nothing else live.  walk_kernel: one request per lane, the same group_walks code.
+// walk_pool_kernel: persistent waves, one walk step (a Node4 visit or a leaf) per lane per
+// iteration, and a lane whose walk ends takes the next request from a global counter, so
+// the wave's lanes stay busy to the end of the list.  Same candidate set, same
+// lexicographic minimum, same gate certification: the results equal group_walks'.
+#ifndef PTMI_WALK_WAVES
+#define PTMI_WALK_WAVES 5
+#endif
+template <bool A>
+__global__ __launch_bounds__(kBlock, PTMI_WALK_WAVES) void walk_kernel(DevScene S, const WalkReq* __restrict__ req,
+                                                                      uint32_t n, WalkRes* __restrict__ res) {
+    __shared__ int stk_lds[kStack * kStkStride];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const WalkReq q = req[i];
+    Hit h{q.t, q.pk, -1, -1, 0.0, 0.0};
+    group_walks<A>(S, lds_ptr(stk_lds + threadIdx.x), mk(q.o[0], q.o[1], q.o[2], 1.0), mk(q.d[0], q.d[1], q.d[2], 0.0), h);
+    res[i] = WalkRes{h.t, h.pk, h.tri, h.ti, 0, h.u, h.v};
+}
+
+#ifndef PTMI_WALK_REFILL
+#define PTMI_WALK_REFILL 16  // lanes without a walk that trigger the wave's finish-and-refill step
+#endif
+template <bool A>
+__global__ __launch_bounds__(kBlock, PTMI_WALK_WAVES) void walk_pool_kernel(DevScene S,
+                                                                           const WalkReq* __restrict__ req,
+                                                                           uint32_t n, WalkRes* __restrict__ res,
+                                                                           uint32_t* __restrict__ next) {
+    __shared__ int stk_lds[kStack * kStkStride];
+    const int lane = threadIdx.x;
+    LdsInt* stk = lds_ptr(stk_lds + lane);
+    const int j_end = S.run_end[4];
+    // Lane phases: kIdle (no request), kWalk (walking object j of request ri), kDone (every
+    // object walked: the gate check, barycentrics and result store are pending), kDrained
+    // (the list is exhausted).  Finishing and refilling run for all such lanes of the wave
+    // together, once PTMI_WALK_REFILL of them wait (their FP64 work then runs on many
+    // lanes), or when no lane walks.
+    enum : int { kIdle = 0, kWalk = 1, kDone = 2, kDrained = 3 };
+    int phase = kIdle;
+    uint32_t ri = 0;
+    int j = 0, cur = kEmptyChild, sp = 0, vchain = -1;
+    bool cert = false;
+    d4 o = mk(0.0, 0.0, 0.0, 1.0), d = mk(0.0, 0.0, 0.0, 0.0);
+    WalkRay W{};
+    float lim = 0.0f;
+    Hit h{1024.0, -1, -1, -1, 0.0, 0.0};
+    // The walk of the first group object from jj on whose hull the segment [eps, best]
+    // can meet; kDone when none is left.
+    auto start_object = [&](int jj) {
+        const WalkReq& q = req[ri];
+        const d4 ro = mk(q.o[0], q.o[1], q.o[2], 1.0), rd = mk(q.d[0], q.d[1], q.d[2], 0.0);
+        for (; jj < j_end; jj++) {
+            const DevObject& ob = S.objs[jj];
+            o = xpt<A>(ob.inv, ob.st, ro);
+            d = xdir<A>(ob.inv, ob.st, rd);
+            const d4 r = mk(rcp_walk(d.x), rcp_walk(d.y), rcp_walk(d.z), 0.0);
+            const RootRec& R = S.root_rec[ob.child_base];  // one traversal index per group object
+            double tn;
+            if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1], R.hull_mx[2],
+                         h.t + prune_margin(h.t), tn))
+                continue;
+            W = walk_setup(o, r, R);
+            lim = walk_limit(h.t);
+            cur = R.entry;
+            sp = 0;
+            vchain = -1;
+            break;
+        }
+        j = jj;
+        phase = jj < j_end ? kWalk : kDone;
+    };
+    for (;;) {
+        const uint64_t wait_m = __ballot(phase == kIdle || phase == kDone);
+        const bool any_walk = __any(phase == kWalk);
+        if (__popcll(wait_m) >= PTMI_WALK_REFILL || (wait_m != 0 && !any_walk)) {
+            if (phase == kDone) {  // the gate check (group_walks), barycentrics, result
+                const WalkReq& q = req[ri];
+                const d4 ro = mk(q.o[0], q.o[1], q.o[2], 1.0), rd = mk(q.d[0], q.d[1], q.d[2], 0.0);
+                if (h.tri >= 0 && !cert) {
+                    const DevObject& ob = S.objs[hit_obj(h)];
+                    if (!verify_chain(S, S.tris[h.ti].chain, xpt<A>(ob.inv, ob.st, ro), xdir<A>(ob.inv, ob.st, rd))) {
+                        h = Hit{q.t, q.pk, -1, -1, 0.0, 0.0};  // the eager walks
+                        group_walks_impl<A, true>(S, stk, ro, rd, h, cert);
+                    }
+                }
+                if (h.tri >= 0) {
+                    const DevObject& ob = S.objs[hit_obj(h)];
+                    tri_uv(S.tris[h.ti], xpt<A>(ob.inv, ob.st, ro), xdir<A>(ob.inv, ob.st, rd), h.u, h.v);
+                }
+                res[ri] = WalkRes{h.t, h.pk, h.tri, h.ti, 0, h.u, h.v};
+                phase = kIdle;
+            }
+            // refill: one atomic for the wave, each waiting lane takes the next request
+            const uint64_t im = __ballot(phase == kIdle);
+            const int first = __ffsll((long long)im) - 1;
+            uint32_t base = 0;
+            if (lane == first) base = atomicAdd(next, (uint32_t)__popcll(im));
+            base = __shfl(base, first);
+            if (phase == kIdle) {
+                ri = base + __popcll(im & ((1ull << lane) - 1));
+                if (ri < n) {
+                    const WalkReq& q = req[ri];
+                    h = Hit{q.t, q.pk, -1, -1, 0.0, 0.0};
+                    cert = false;
+                    start_object(S.run_end[3]);
+                } else {
+                    phase = kDrained;
+                }
+            }
+        }
+        if (!__any(phase == kWalk || phase == kDone)) break;
+        if (phase == kWalk) {  // one walk step of object j (walk_index's loop body)
+            bool down = false;
+            if (cur >= 0) {
+                int nxt;
+                down = node_visit(S, stk, cur, sp, W, lim, nxt);
+                if (down) cur = nxt;
+            } else if (cur != kEmptyChild) {
+                leaf_visit<false>(S, -cur - 1, j, S.objs[j].key, o, d, h, vchain);
+                lim = walk_limit(h.t);
+            }
+            if (!down) {
+                if (sp > 0) {
+                    cur = stk[(--sp) * kStkStride];
+                } else {  // object j walked: certify a winner from it, then the next object
+                    if (h.tri >= 0 && hit_obj(h) == j) cert = chain_certified(S, S.tris[h.ti].chain, o, d, h.t);
+                    start_object(j + 1);
+                }
+            }
+        }
+    }
+}
+
+hipError_t launch_walk(const DevScene& S, int flags, int mode, const WalkReq* req, uint32_t n, WalkRes* res,
+                       uint32_t* next, uint32_t grid, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    if ((flags & (F_PROJ | F_TEX)) || !(flags & F_GROUPS)) return hipErrorInvalidValue;  // affine mesh scenes
+    if (mode == 0) {
+        hipLaunchKernelGGL(walk_kernel<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, S, req, n, res);
+    } else {
+        hipLaunchKernelGGL(walk_pool_kernel<true>, dim3(grid), dim3(kBlock), 0, st, S, req, n, res, next);
+    }
+    return hipGetLastError();
+}
+
+const void* walk_kernel_symbol(int mode) {
+    return mode == 0 ? reinterpret_cast<const void*>(&walk_kernel<true>)
+                     : reinterpret_cast<const void*>(&walk_pool_kernel<true>);
+}
+
+#if PTMI_CAPTURE
+hipError_t capture_setup(WalkReq* req, WalkRes* res, uint32_t cap) {
+    unsigned z = 0;
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(ptmi_cap_req), &req, sizeof(req));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(ptmi_cap_res), &res, sizeof(res));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(ptmi_cap_max), &cap, sizeof(cap));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(ptmi_cap_n), &z, sizeof(z));
+    return e;
+}
+hipError_t capture_count(uint32_t* n) { return hipMemcpyFromSymbol(n, HIP_SYMBOL(ptmi_cap_n), sizeof(*n)); }
+#else
+hipError_t capture_setup(WalkReq*, WalkRes*, uint32_t) { return hipErrorNotSupported; }
+hipError_t capture_count(uint32_t*) { return hipErrorNotSupported; }
+#endif
 
 // DoF aperture offsets sunflower(S, 2, n) for n in [0, S) (tracer.cl:221-248,
 // 766): a per-frame table, same arithmetic as the reference.

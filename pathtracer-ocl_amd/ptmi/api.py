@@ -30,7 +30,7 @@ EXPORTS = ("ptmi_trace", "ptmi_device_count", "ptmi_device_name", "ptmi_scene_cr
            "ptmi_scene_size", "ptmi_scene_render", "ptmi_finalize", "ptmi_fill_seeds", "ptmi_build_info",
            "ptmi_scene_set_timing", "ptmi_scene_kernel_time", "ptmi_trace_multi", "ptmi_scene_create_textured",
            "ptmi_trace_multi_timed", "ptmi_sample_split_point", "ptmi_combine_frames",
-           "ptmi_scene_set_rng")
+           "ptmi_scene_set_rng", "ptmi_index_stats")
 
 
 class MultiTiming(ctypes.Structure):
@@ -103,6 +103,9 @@ def load_library(path=None):
     lib.ptmi_scene_kernel_time.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u32), cp, sz]
     lib.ptmi_build_info.restype = cp
     lib.ptmi_build_info.argtypes = []
+    if hasattr(lib, "ptmi_index_stats"):
+        lib.ptmi_index_stats.restype = i32
+        lib.ptmi_index_stats.argtypes = [vp, u32, vp, u32, vp, u32, vp, ctypes.POINTER(ctypes.c_double), i32, cp, sz]
     if path is None:
         _lib = lib
     return lib
@@ -201,6 +204,17 @@ def combine_frames(parts_ptr, n_parts, n_pixels, out_ptr, samples, stream=0):
     _check(load_library().ptmi_combine_frames(ctypes.c_void_p(parts_ptr), int(n_parts), int(n_pixels),
                                               ctypes.c_void_p(out_ptr), int(samples), ctypes.c_void_p(stream),
                                               err, len(err)), err)
+
+
+def index_stats(objects, triangles, groups, camera):
+    """ptmi_index_stats (host only): summary of the traversal index the library builds
+    for these records -- {nodes4, slots, box_area, inf_bounds, max_scale_exp, roots}."""
+    objects, triangles, groups, camera = _records(objects, triangles, groups, camera)
+    out = (ctypes.c_double * 6)()
+    err = ctypes.create_string_buffer(1024)
+    _check(load_library().ptmi_index_stats(_ptr(objects), len(objects), _ptr(triangles), len(triangles),
+                                           _ptr(groups), len(groups), _ptr(camera), out, 6, err, len(err)), err)
+    return dict(zip(("nodes4", "slots", "box_area", "inf_bounds", "max_scale_exp", "roots"), list(out)))
 
 
 def sample_split_point(g, n, samples):

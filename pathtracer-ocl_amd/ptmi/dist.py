@@ -16,7 +16,8 @@ partial framebuffers:
 
 Either way the frame is the elementwise SUM of the partial framebuffers
 (ptmi_scene_render writes RGB sums, A = number of samples), reduced with one
-all_reduce(SUM) of W*H*4 doubles and normalised on device (ptmi_finalize).
+reduce(SUM) of W*H*4 doubles onto rank 0 (reduce_frame_to) and normalised there on
+device (ptmi_finalize).
 For the tile split the sum is exact (x + 0 = x); for the sample split it
 differs from a one-GPU render only by FP64 summation order (~1e-16 relative).
 """

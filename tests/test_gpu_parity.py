@@ -267,6 +267,25 @@ def test_hip_matches_live_reference_adversarial_bvh(kind, ap):
     assert err < 1e-12, "%s: L-inf %.3e vs live reference" % (kind, err)
 
 
+@pytest.mark.parametrize("offset,scale", [((1.0e4, 0.0, 0.0), 1.0), ((-3.0e4, 2.0e4, 7.5e3), 1.0),
+                                          ((1.0e9, 0.0, -2.0e9), 3.0e5)])
+def test_hip_matches_live_reference_moved_mesh(offset, scale):
+    """The teapot moved in its object space far from the origin and / or scaled past
+    binary16's range (tests/moved_mesh.py): the traversal index's per-root frame
+    (ptmi_bvh.cpp RootRec ctr / sc) must stay conservative."""
+    if not pyoracle.ref_available():
+        pytest.skip("oracle/_ref not built")
+    from tests.moved_mesh import moved
+    w, h, spp = 64, 48, 3
+    objs, tris, grps, cam = scene_inputs("teapot", w, h)
+    objs, tris, grps = moved(objs, tris, grps, offset=offset, scale=scale)
+    seeds = layout.seeds_go_float64(w * h, 640)
+    ref = pyoracle.ref_trace(objs, tris, grps, cam, spp, seeds)
+    out = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    err = np.abs(out - ref).max()
+    assert err < 1e-12, "offset %s scale %g: L-inf %.3e vs live reference" % (offset, scale, err)
+
+
 @pytest.mark.parametrize("scene,ap", [("transparency", 0.0), ("transparency_quad_lights", 0.15),
                                       ("reflection", 0.0), ("transparent_teapot", 0.0)])
 def test_cpu_oracle_matches_live_reference_materials(scene, ap):

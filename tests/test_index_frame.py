@@ -1,0 +1,53 @@
+"""The traversal index's per-root frame (ptmi_bvh.cpp, RootRec ctr / sc): Node4
+bounds are binary16 values of (bound - ctr) / 2^s, so a mesh far from the origin or larger
+than binary16's range keeps boxes as tight as the same mesh at the origin.  Host only
+(ptmi_index_stats builds the index on the CPU); the GPU parity of moved meshes against the
+live reference is in tests/test_gpu_parity.py."""
+import pytest
+
+from ptmi import api
+from tests.moved_mesh import moved
+from tests.scene_inputs import scene_inputs
+
+
+@pytest.fixture(scope="module")
+def teapot():
+    return scene_inputs("teapot", 64, 48)
+
+
+def _stats(objs, tris, grps, cam):
+    return api.index_stats(objs, tris, grps, cam)
+
+
+def test_index_stats_of_the_teapot(teapot):
+    st = _stats(*teapot)
+    assert st["roots"] == 1 and st["nodes4"] > 100 and st["slots"] > st["nodes4"]
+    assert st["inf_bounds"] == 0 and st["max_scale_exp"] == 0
+
+
+@pytest.mark.parametrize("offset,tol", [((1.0e3, 0.0, 0.0), 0.005), ((1.0e4, 0.0, 0.0), 0.02),
+                                        ((-3.0e4, 2.0e4, 7.5e3), 0.05)])
+def test_offset_mesh_keeps_its_boxes(teapot, offset, tol):
+    """Translated in object space by 1e3-3e4 units (an OBJ in millimetres, say): the
+    decoded boxes' total surface area stays close to the mesh's at the origin.  In a frame
+    at the origin the binary16 rounding near |x| = 1e4 alone is 4-8 units on this mesh,
+    which is ~7 units across, and past 65504 every bound on that axis is infinite.  What
+    is left is the index's widening, 1e-7 x the largest |coordinate| (it covers hit-point
+    rounding, which grows with the coordinates): 0.1 % / 1.5 % / 4.4 % more box area
+    here."""
+    objs, tris, grps, cam = teapot
+    base = _stats(objs, tris, grps, cam)
+    st = _stats(*moved(objs, tris, grps, offset=offset), cam)
+    assert st["nodes4"] == base["nodes4"] and st["inf_bounds"] == 0
+    assert abs(st["box_area"] / base["box_area"] - 1.0) < tol, (st, base)
+
+
+@pytest.mark.parametrize("scale,offset", [(1.0e5, (0.0, 0.0, 0.0)), (3.0e5, (1.0e9, 0.0, -2.0e9))])
+def test_large_mesh_gets_finite_scaled_bounds(teapot, scale, offset):
+    """Scaled past binary16's range (extent up to ~1e7 units): the root scale 2^s keeps
+    every bound finite, and box areas scale with the mesh (within 2 %)."""
+    objs, tris, grps, cam = teapot
+    base = _stats(objs, tris, grps, cam)
+    st = _stats(*moved(objs, tris, grps, offset=offset, scale=scale), cam)
+    assert st["inf_bounds"] == 0 and st["max_scale_exp"] > 0, st
+    assert abs(st["box_area"] / (base["box_area"] * scale * scale) - 1.0) < 0.02, (st, base)

@@ -12,6 +12,10 @@ Inputs in the round directory, per config c in c2..c5 (all optional):
 import argparse
 import json
 import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import build_id  # noqa: E402
 
 KEYS = {"c2": "c2_reference_1280x960", "c3": "c3_reference_dof_1280x960", "c4": "c4_teapot_1280x960",
         "c5": "c5_gopher_1280x960"}
@@ -30,9 +34,14 @@ def main():
     ap.add_argument("round_dir")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles",
                                                   "pmc_measured.json"))
+    ap.add_argument("--spp", type=int, default=2048, help="samples per pixel of the profiled frames")
+    ap.add_argument("--build", default=None, help="build id of the profiled library (default: this tree's)")
     a = ap.parse_args()
-    out = {"what": "rocprofv3 PMC measurements per trace_kernel launch of one full 2048-spp frame, "
-                   "frozen from %s by tools/pmc_freeze.py" % os.path.normpath(a.round_dir),
+    out = {"what": "rocprofv3 PMC measurements per trace_kernel launch of one full %d-spp frame, "
+                   "frozen from %s by tools/pmc_freeze.py" % (a.spp, os.path.normpath(a.round_dir)),
+           "build": a.build or build_id(), "spp": a.spp,
+           "build_note": "bench.py reports these counters only for the build they were measured on "
+                         "(bench.build_id: a hash of the kernel sources)",
            "workloads": {}}
     for c, key in KEYS.items():
         w = {}
