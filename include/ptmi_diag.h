@@ -25,6 +25,13 @@ int ptmi_diag_capture_count(uint32_t* n, char* err, size_t err_len);
 int ptmi_diag_walk(ptmi_scene* s, int mode, const void* req_dev, uint32_t n, void* res_dev,
                    uint32_t* counter_dev, void* hip_stream, float* ms, char* err, size_t err_len);
 
+/* Mesh-scene execution form: enable != 0 renders affine mesh scenes in the split form
+ * (trace_split_kernel + walk_split_kernel, pass by pass), 0 (the default) in the
+ * one-kernel form (trace_kernel with in-loop walk phases).  Both give the same image
+ * for the same chunking.  ptmi_diag_split_passes: passes of the last split render. */
+int ptmi_diag_set_split(ptmi_scene* s, int enable);
+int ptmi_diag_split_passes(const ptmi_scene* s);
+
 #ifdef __cplusplus
 }
 #endif

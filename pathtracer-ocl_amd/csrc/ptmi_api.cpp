@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -35,6 +36,12 @@ hipError_t launch_hemi_table(double* out, int* mismatch, hipStream_t st);
 hipError_t launch_combine(const double* parts, uint32_t nparts, size_t npix, double* out, uint32_t samples,
                           hipStream_t st);
 const void* trace_kernel_symbol(int flags);
+bool split_supported(int flags);
+const void* trace_split_symbol(int flags);
+const void* walk_split_symbol();
+hipError_t launch_split_pass(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const SplitBufs& B,
+                             const double* seeds, const double* sunf, double* part, uint32_t walk_grid,
+                             hipStream_t st);
 int trace_block_threads(int flags);
 int trace_tiles_per_block(int flags);
 }  // namespace ptmi
@@ -60,6 +67,19 @@ struct ptmi_scene {
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pending (start, stop) pairs
     std::vector<hipEvent_t> spare;
+    // Split execution of affine mesh scenes (ptmi_kernels.hip trace_split_kernel): a measured
+    // alternative, off by default (3.3x slower than the one-kernel form on C4);
+    // PTMI_SPLIT=1 or ptmi_diag_set_split(s, 1) selects it.
+    int split = 0;
+    uint32_t split_chunk = 64;       // samples per pixel-chunk (PTMI_SPLIT_CHUNK)
+    uint32_t split_per_lane = 4;     // slots per tracer lane slot (PTMI_SPLIT_SLOTS)
+    uint32_t split_sync = 8;         // passes between completion checks (PTMI_SPLIT_SYNC)
+    uint32_t split_budget = 4;       // samples a slot starts per pass (PTMI_SPLIT_BUDGET)
+    SplitBufs sb{};
+    void* split_mem = nullptr;
+    size_t split_bytes = 0;
+    uint32_t* split_host = nullptr;  // pinned: the request count read back at a check
+    uint32_t split_passes = 0;       // passes of the last split render (diagnostics)
 };
 
 namespace {
@@ -494,11 +514,108 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     if (const char* t = getenv("PTMI_TAIL_TILES")) s->tail_tiles = (uint32_t)atoi(t);  // testing: small frames with whole tiles
     if (const char* t = getenv("PTMI_TAIL_ITEMS")) s->tail_items = (uint32_t)std::max(1, atoi(t));  // tuning
     if (const char* t = getenv("PTMI_MESH_ITEMS")) s->mesh_items = (uint32_t)std::max(1, atoi(t));  // tuning
+    if (const char* t = getenv("PTMI_SPLIT")) s->split = atoi(t) != 0;
+    if (const char* t = getenv("PTMI_SPLIT_CHUNK")) s->split_chunk = (uint32_t)std::max(1, atoi(t));
+    if (const char* t = getenv("PTMI_SPLIT_SLOTS")) s->split_per_lane = (uint32_t)std::max(1, atoi(t));
+    if (const char* t = getenv("PTMI_SPLIT_SYNC")) s->split_sync = (uint32_t)std::max(1, atoi(t));
+    if (const char* t = getenv("PTMI_SPLIT_BUDGET")) s->split_budget = (uint32_t)std::max(1, atoi(t));
     s->dev.n_tri = hs.n_tri;
     s->dev.cam = hs.cam;
     SCENE_TRY(resident_waves(s));
 #undef SCENE_TRY
     *out = s;
+    return PTMI_OK;
+}
+
+
+// Split execution of an affine mesh scene (ptmi_kernels.hip trace_split_kernel): pixel-chunks
+// of chunk_len samples over every owned tile, traced pass by pass by a pool of L path slots
+// (L = the tracer's resident lanes x split_per_lane), each pass followed by the walks it
+// asked for, until a pass asks for none.  Chunk records go to `part` in the WorkPlan's
+// chunk-major layout (store_sums' records), summed by reduce_chunks_kernel as for the
+// one-kernel form's chunk items.
+int render_split(ptmi_scene* s, uint32_t samples, const WorkPlan& wp, const double* seeds, double* sums,
+                 hipStream_t st, char* err, size_t err_len) {
+    const int flags = s->flags;
+    hipDeviceProp_t p;
+    HIP_TRY(hipGetDeviceProperties(&p, s->device));
+    int per_cu = 0, walk_cu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_split_symbol(flags), 64, 0));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&walk_cu, walk_split_symbol(), 64, 0));
+    const uint32_t waves = (uint32_t)std::max(1, per_cu) * (uint32_t)p.multiProcessorCount;
+    const uint32_t walk_grid = (uint32_t)std::max(1, walk_cu) * (uint32_t)p.multiProcessorCount;
+    const uint32_t per_wave = 64u * s->split_per_lane;
+    const uint64_t n_items64 = (uint64_t)wp.n_tail * 64u * wp.nchunks;
+    if (n_items64 >= 0xFFFFFFF0ull) {
+        set_err(err, err_len, "split render: %llu pixel-chunks exceed 32-bit ids", (unsigned long long)n_items64);
+        return PTMI_ERR_UNSUPPORTED;
+    }
+    const uint32_t n_items = (uint32_t)n_items64;
+    // Slots: the tracer's resident waves x per_wave, but no more than there are pixel-chunks.
+    uint32_t L = waves * per_wave;
+    L = std::max<uint32_t>(64, std::min<uint32_t>(L, (n_items + 63) / 64 * 64));
+    const uint32_t n_waves = (L + per_wave - 1) / per_wave;
+    const size_t need = (size_t)L * (kSlotBytes + 4) + (size_t)n_waves * 12 + 512;
+    if (need > s->split_bytes) {
+        if (s->split_mem) {
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipFree(s->split_mem));
+            s->split_mem = nullptr;
+            s->split_bytes = 0;
+        }
+        HIP_TRY(hipMalloc(&s->split_mem, need));
+        s->split_bytes = need;
+    }
+    if (!s->split_host) HIP_TRY(hipHostMalloc((void**)&s->split_host, 64, hipHostMallocDefault));
+    char* m = (char*)s->split_mem;
+    SplitBufs& B = s->sb;
+    B.rec = m;
+    m += (size_t)L * kSlotBytes;
+    B.req = (uint32_t*)m;
+    m += (size_t)L * 4;
+    B.seg = (uint32_t*)m;
+    m += (size_t)n_waves * 4;
+    B.wcl = (uint32_t*)m;
+    m += (size_t)n_waves * 8;
+    B.cnt = (uint32_t*)m;
+    B.L = L;
+    B.per_wave = per_wave;
+    B.n_items = n_items;
+    B.budget = s->split_budget;
+    HIP_TRY(hipMemset2DAsync(B.rec + offsetof(SplitRec, u), kSlotBytes, 0xFF, 4, L, st));  // every slot kSlotFree
+    HIP_TRY(hipMemsetAsync(B.cnt, 0, 16, st));
+    HIP_TRY(hipMemsetAsync(B.wcl, 0, (size_t)n_waves * 8, st));  // no block claimed yet
+    // A bound no render reaches: every pass finishes or advances at least one pixel-chunk
+    // by a bounce, so a runaway loop means a bug; fail instead of spinning.
+    const uint64_t max_passes = ((uint64_t)n_items / L + 1) * 11ull * wp.chunk_len + 1024;
+    uint32_t pass = 0;
+    for (;;) {
+        HIP_TRY(hipMemsetAsync(B.cnt, 0, 4, st));  // this pass's request count
+        HIP_TRY(hipMemsetAsync(B.cnt + 2, 0, 4, st));  // and yield count
+        HIP_TRY(launch_split_pass(s->dev, flags, samples, wp, B, seeds, s->sunf, s->partial, walk_grid, st));
+        pass++;
+        if (pass % s->split_sync == 0) {
+            HIP_TRY(hipMemcpyAsync(s->split_host, B.cnt, 12, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            if (s->split_host[0] == 0 && s->split_host[2] == 0 && s->split_host[1] >= n_items) break;
+        }
+        if (pass > max_passes) {
+            set_err(err, err_len, "split render did not finish in %u passes", pass);
+            return PTMI_ERR_HIP;
+        }
+    }
+    s->split_passes = pass;
+    if (getenv("PTMI_SPLIT_DEBUG")) {  // DIAGNOSTIC: slot states after the last pass
+        std::vector<uint32_t> it(L);
+        HIP_TRY(hipMemcpy2D(it.data(), 4, B.rec + offsetof(SplitRec, u), kSlotBytes, 4, L, hipMemcpyDeviceToHost));
+        uint32_t cnt[4];
+        HIP_TRY(hipMemcpy(cnt, B.cnt, 16, hipMemcpyDeviceToHost));
+        size_t fr = 0, dead = 0, busy = 0;
+        for (uint32_t v : it) (v == kSlotFree ? fr : v == kSlotDead ? dead : busy)++;
+        fprintf(stderr, "split: L %u items %u passes %u walk_grid %u per_cu %d: free %zu dead %zu busy %zu req %u claims %u walks %u\n",
+                L, n_items, pass, walk_grid, per_cu, fr, dead, busy, cnt[0], cnt[1], cnt[3]);
+    }
+    (void)sums;
     return PTMI_OK;
 }
 
@@ -589,6 +706,8 @@ void ptmi_scene_destroy(ptmi_scene* s) {
         if (b) (void)hipFree(b);
     if (s->partial) (void)hipFree(s->partial);
     if (s->sunf) (void)hipFree(s->sunf);
+    if (s->split_mem) (void)hipFree(s->split_mem);
+    if (s->split_host) (void)hipHostFree(s->split_host);
     for (auto& e : s->events) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
@@ -638,8 +757,23 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     wp.s_end = sample_end;
     wp.tile_stride = tile_stride;
     wp.tile_offset = tile_offset;
+    // Affine mesh scenes in parity mode, when the split form is selected (render_split): pixel-chunks of
+    // split_chunk samples (an explicit `chunks` sets the chunk count as for the one-kernel
+    // form, so both forms then sum the same chunks in the same order).
+    const int kflags = s->flags | (s->rng == PTMI_RNG_XOSHIRO ? 64 : 0);
+    const bool split = s->split && split_supported(kflags) && range > 0;
+    if (split) {
+        uint32_t nch = chunks ? chunks : (range + s->split_chunk - 1) / s->split_chunk;
+        nch = std::max<uint32_t>(1, std::min<uint32_t>(nch, range));
+        wp.chunk_len = (range + nch - 1) / nch;
+        wp.nchunks = (range + wp.chunk_len - 1) / wp.chunk_len;
+        wp.n_whole = 0;
+        wp.n_tail = owned_tiles;
+    }
     uint32_t n_tail = owned_tiles;
-    if (chunks == 0) {
+    if (split) {
+        chunks = wp.nchunks;
+    } else if (chunks == 0) {
         const bool mesh = (s->flags & 1) != 0;  // F_GROUPS
         if (!mesh || s->tail_tiles)
             n_tail = std::min<uint32_t>(owned_tiles, s->tail_tiles ? s->tail_tiles : (uint32_t)(s->resident_waves / 2));
@@ -650,7 +784,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     chunks = std::max<uint32_t>(1, std::min<uint32_t>(chunks, std::max<uint32_t>(range, 1)));
     const uint32_t chunk_len = range == 0 ? 1 : (range + chunks - 1) / chunks;
     chunks = range == 0 ? 1 : (range + chunk_len - 1) / chunk_len;
-    if (chunks == 1) n_tail = 0;  // one chunk: every tile is whole
+    if (chunks == 1 && !split) n_tail = 0;  // one chunk: every tile is whole
     wp.n_whole = owned_tiles - n_tail;
     wp.n_tail = n_tail;
     wp.nchunks = chunks;
@@ -690,8 +824,12 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         s->partial_bytes = need;
     }
     if (ev0) HIP_TRY(hipEventRecord(ev0, st));
-    HIP_TRY(launch_trace(s->dev, s->flags | (s->rng == PTMI_RNG_XOSHIRO ? 64 : 0), samples, wp, seeds_dev, s->sunf,
-                         sums_dev, s->partial, st));
+    if (split) {
+        const int rc = render_split(s, samples, wp, seeds_dev, sums_dev, st, err, err_len);
+        if (rc) return rc;
+    } else {
+        HIP_TRY(launch_trace(s->dev, kflags, samples, wp, seeds_dev, s->sunf, sums_dev, s->partial, st));
+    }
     if (ev1) {
         HIP_TRY(hipEventRecord(ev1, st));
         s->events.emplace_back(ev0, ev1);
@@ -1054,6 +1192,7 @@ extern "C" int ptmi_diag_walk(ptmi_scene* s, int mode, const void* req_dev, uint
         int per_cu = 0;
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, walk_kernel_symbol(1), 64, 0));
         grid = (uint32_t)std::max(1, per_cu) * (uint32_t)p.multiProcessorCount;
+        if (const char* g = getenv("PTMI_WALK_GRID_MULT")) grid *= (uint32_t)std::max(1, atoi(g));  // tuning
         HIP_TRY(hipMemsetAsync(counter_dev, 0, sizeof(uint32_t), st));
     }
     hipEvent_t e0, e1;
@@ -1076,3 +1215,11 @@ extern "C" int ptmi_diag_walk(ptmi_scene* s, int mode, const void* req_dev, uint
     if (ms) *ms = t;
     return PTMI_OK;
 }
+
+extern "C" int ptmi_diag_set_split(ptmi_scene* s, int enable) {
+    if (!s) return PTMI_ERR_ARG;
+    s->split = enable != 0;
+    return PTMI_OK;
+}
+
+extern "C" int ptmi_diag_split_passes(const ptmi_scene* s) { return s ? (int)s->split_passes : -1; }

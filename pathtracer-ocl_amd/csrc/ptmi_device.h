@@ -183,6 +183,38 @@ struct alignas(16) WalkRes {
 };
 static_assert(sizeof(WalkRes) == 40 || sizeof(WalkRes) == 48, "WalkRes size");
 
+// Split execution of mesh scenes (trace_split_kernel + walk_split_kernel, round 4): a
+// pool of L path slots in HBM, structure of arrays.  A slot works on one pixel-chunk
+// (pixel x sample range) at a time, its samples in order; when its ray needs a BVH walk
+// the tracer saves the path here and appends the slot to the request list, the walker
+// walks the list, and the next tracer pass resumes the path with the result.
+struct SplitBufs {
+    char* rec;     // [L] slot records of kSlotBytes (SplitRec), one slot's state on 4 cache lines
+    uint32_t* req; // [L]: this pass's walk requests (slot ids); tracer wave w appends to its own
+                   // segment [w * per_wave, + seg[w]) -- no atomics on a shared counter
+    uint32_t* seg; // [L / per_wave]: requests in each wave's segment
+    uint32_t* wcl; // [2 L / per_wave]: each wave's claimed block of pixel-chunks [next, end), kept
+                   // from pass to pass (a block left half used at a pass's end is not lost)
+    uint32_t* cnt; // [0] requests of the pass, [1] next pixel-chunk block to claim, [2] yields of the pass
+    uint32_t L, per_wave, n_items, budget;  // budget: samples a slot starts per pass before it yields
+};
+// One slot (SplitBufs::rec): d = ro xyz, rd xyz, mask rgb, accumColor rgb, pixel-chunk sums rgb,
+// best t; u = pixel-chunk id (or kSlotFree / kSlotDead), sample index, path flags, best pk;
+// f = fgi, fgi2; res = the walk result.  Records rather than arrays per field: a resume or a
+// save touches one slot's lines, not 20 arrays (TLB, load instructions).
+struct alignas(256) SplitRec {
+    double d[16];
+    uint32_t u[4];
+    float f[2];
+    uint32_t pad[2];
+    WalkRes res;
+};
+constexpr size_t kSlotBytes = sizeof(SplitRec);
+static_assert(kSlotBytes == 256, "SplitRec must stay 256 B");
+constexpr int kSplitD = 16;
+constexpr int kSplitU = 4;
+constexpr uint32_t kSlotFree = 0xFFFFFFFFu, kSlotDead = 0xFFFFFFFEu;
+
 constexpr int kTile = 8;          // a wave64 covers an 8x8 pixel tile
 
 // One launch's work items (trace_kernel, by value).  The owned tiles are

@@ -2219,6 +2219,330 @@ __global__ __launch_bounds__(kBlock, PTMI_WALK_WAVES) void walk_pool_kernel(DevS
     }
 }
 
+// ---- Split execution of mesh scenes (round 4) -------------------------------------
+// The mesh kernel above keeps every path in registers and walks the BVH in wave-wide walk
+// phases: ~24 parked lanes walk while the others wait, and parked lanes idle through the
+// primitive and shading phases.  Measured on the walks of real frames (tools/walk_bench.py,
+// profiles/r4/walk_kernel): the same walks cost 2.1x less in a standalone kernel, and the
+// mesh kernel without its walks (the mesh made invisible, hull culls kept) runs C4 / C5 in
+// 286 / 330 ms instead of 627 / 966 ms.  The split form runs those two halves as separate
+// kernels over a pool of path slots in HBM (SplitBufs), pass by pass:
+//   trace_split_kernel: each wave owns B.per_wave slots and hands them to its lanes; a lane
+//     resumes a slot's path (applying the walk result of the previous pass), traces it --
+//     primitives, hull culls, shading, its next samples -- until its ray needs a walk, then
+//     saves the path and the primitive best, appends the slot to the request list and takes
+//     the wave's next slot.  A slot whose pixel-chunk is finished claims the next one.
+//   walk_split_kernel: group_walks for every request of the pass (the same code as the mesh
+//     kernel's walk phases), result to the slot.
+// Per slot the samples of a pixel-chunk run in order with the reference's arithmetic, and
+// chunk sums go to the same partial records as the mesh kernel's chunk items, so the frame
+// equals a mesh-kernel render with the same chunk length bit for bit.
+#ifndef PTMI_WAVES_SPLIT
+#define PTMI_WAVES_SPLIT 5
+#endif
+#ifndef PTMI_SPLIT_BATCH
+#define PTMI_SPLIT_BATCH 16  // waiting lanes that trigger a batched slot / claim / camera step
+#endif
+// A slot yields after starting B.budget samples in one pass (saved at a sample boundary,
+// resumed by the next pass): every wave then does about the same work per pass, so a pass
+// is not as long as its luckiest wave's run of walk-free samples.
+static constexpr uint32_t kFlagYield = 1u << 9;  // path flags: saved at a sample boundary, no walk pending
+// Pixel-chunks are claimed by the wave in blocks of one tile-chunk (64 consecutive ids, the
+// 64 pixels of one tile for one sample chunk), one global atomic per block.  (One atomic
+// per claim, and one per batch of walk requests, on shared counters had left the split
+// kernel's waves waiting on the atomic unit most of the pass.)
+static constexpr uint32_t kClaimBlock = 64;
+template <int FL>
+__global__ __launch_bounds__(kBlock, PTMI_WAVES_SPLIT) void trace_split_kernel(DevScene S, uint32_t samples,
+                                                                              WorkPlan WP, SplitBufs B,
+                                                                              const double* __restrict__ seeds,
+                                                                              const double* __restrict__ sunf,
+                                                                              double* __restrict__ part) {
+    static_assert((FL & F_GROUPS) && !(FL & (F_PROJ | F_TEX | F_XRNG)), "affine parity mesh scenes");
+    constexpr bool A = true;
+    constexpr bool kDof = (FL & F_DOF) != 0;
+    __shared__ double acc_lds[3 * kBlock];
+    const int lane = threadIdx.x;
+    double* acc = acc_lds + lane;
+    // The wave's next slot to hand out: wave-uniform, so every lane keeps its own copy and
+    // advances it by the same ballot count (a counter in LDS written by one lane and read
+    // by others without synchronisation had let lanes see stale values).
+    uint32_t next_slot = 0;
+    // Wave-uniform counters, kept identical in every lane: the claimed block of
+    // pixel-chunks [cl_next, cl_end), this pass's walk requests and yields.
+    uint32_t cl_next = B.wcl[2 * blockIdx.x], cl_end = B.wcl[2 * blockIdx.x + 1], n_req = 0, n_yield = 0;
+    bool claims_done = false;
+    const uint32_t L = B.L;
+    const uint32_t base = blockIdx.x * B.per_wave;
+    const uint32_t end = min(base + B.per_wave, L);
+    const int W = S.cam.width, H = S.cam.height;
+    const int tiles_x = (W + kTile - 1) / kTile, tiles_y = (H + kTile - 1) / kTile;
+    const uint32_t n_tiles = max(WP.n_tail, 1u);
+    enum : int { kNoSlot = 0, kClaim = 1, kNeedCam = 2, kTrace = 3, kReady = 4, kExhausted = 5 };
+    int mode = kNoSlot;
+    uint32_t slot = 0, q = 0, n_cur = 0, c_end = 0, spent = 0;
+    int px = 0, py = 0;
+    float fgi = 0.0f;
+    PathState P;
+    start_path<A, kDof>(P, mk(0.0, 0.0, 0.0, 1.0), mk(0.0, 0.0, 0.0, 0.0));
+    Hit h{1024.0, -1, -1, -1, 0.0, 0.0};
+    // Pixel-chunk q -> pixel and sample range; false for a pixel outside the image.
+    auto decode = [&](uint32_t qq, uint32_t& c0) -> bool {
+        const uint32_t l = qq & 63u, tc = qq >> 6, c = tc / n_tiles, tk = tc - c * n_tiles;
+        const uint32_t tile = WP.tile_offset + tk * WP.tile_stride;
+        px = (int)(tile % (uint32_t)tiles_x) * kTile + (int)(l & 7u);
+        py = (int)(tile / (uint32_t)tiles_x) * kTile + (int)(l >> 3);
+        c0 = WP.s_begin + c * WP.chunk_len;
+        c_end = min(WP.s_end, c0 + WP.chunk_len);
+        return tile < (uint32_t)(tiles_x * tiles_y) && px < W && py < H;
+    };
+    auto R = [&]() -> SplitRec& { return reinterpret_cast<SplitRec*>(B.rec)[slot]; };
+    auto dget = [&](int k) -> double& { return R().d[k]; };
+    auto uget = [&](int k) -> uint32_t& { return R().u[k]; };
+    for (;;) {
+        const bool tr = mode == kTrace || mode == kReady;
+        // A. Lanes without a slot take the wave's next ones (batched).
+        {
+            const uint64_t m = __ballot(mode == kNoSlot);
+            if (m && (__popcll(m) >= PTMI_SPLIT_BATCH || !__any(tr || mode == kNeedCam || mode == kClaim))) {
+                const uint32_t b0 = next_slot;
+                next_slot += (uint32_t)__popcll(m);
+                if (mode == kNoSlot) {
+                    const uint32_t k = base + b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+                    if (k >= end) {
+                        mode = kExhausted;
+                    } else {
+                        slot = k;
+                        const uint32_t it = uget(0);
+                        if (it == kSlotFree) {
+                            spent = 0;
+                            mode = kClaim;
+                        } else if (it != kSlotDead && (uget(2) & kFlagYield)) {  // yielded between samples
+                            q = it;
+                            uint32_t c0;
+                            decode(q, c0);
+                            n_cur = uget(1);
+                            acc[0 * kBlock] = dget(12), acc[1 * kBlock] = dget(13), acc[2 * kBlock] = dget(14);
+                            fgi = R().f[0];
+                            spent = 0;
+                            mode = kNeedCam;
+                        } else if (it != kSlotDead) {  // a path waiting for its walk result: resume it
+                            q = it;
+                            spent = 0;
+                            uint32_t c0;
+                            decode(q, c0);
+                            n_cur = uget(1);
+                            const uint32_t fl = uget(2);
+                            P.ro = mk(dget(0), dget(1), dget(2), 1.0);
+                            P.rd = mk(dget(3), dget(4), dget(5), 0.0);
+                            P.mr = dget(6), P.mg = dget(7), P.mb = dget(8);
+                            P.ar = dget(9), P.ag = dget(10), P.ab = dget(11);
+                            acc[0 * kBlock] = dget(12), acc[1 * kBlock] = dget(13), acc[2 * kBlock] = dget(14);
+                            P.b = fl & 15u, P.effective = (fl >> 4) & 7u;
+                            P.inside = (fl >> 7) & 1u, P.done = (fl >> 8) & 1u, P.dead = false;
+                            fgi = R().f[0];
+                            const WalkRes r = R().res;
+                            h = Hit{r.t, r.pk, r.tri, r.ti, r.u, r.v};
+                            mode = kReady;
+                        }
+                    }
+                }
+            }
+        }
+        // B. Slots without a pixel-chunk claim the next ones (batched, one atomic).
+        {
+            const uint64_t m = __ballot(mode == kClaim);
+            if (m && (__popcll(m) >= PTMI_SPLIT_BATCH || !__any(tr || mode == kNeedCam))) {
+                if (cl_next >= cl_end && !claims_done) {  // the wave's next block (one atomic)
+                    const int first = __ffsll((long long)m) - 1;
+                    uint32_t b0 = 0;
+                    if (lane == first) b0 = atomicAdd(&B.cnt[1], kClaimBlock);
+                    b0 = __shfl(b0, first);
+                    cl_next = b0;
+                    cl_end = min(b0 + kClaimBlock, B.n_items);
+                    claims_done = b0 >= B.n_items;
+                }
+                const uint32_t avail = cl_next < cl_end ? cl_end - cl_next : 0u;
+                const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1));
+                cl_next += min(avail, (uint32_t)__popcll(m));
+                if (mode == kClaim && rank >= avail) {
+                    if (claims_done) {  // every pixel-chunk is claimed: the slot is done for good
+                        uget(0) = kSlotDead;
+                        mode = kNoSlot;
+                    }  // else: claims again from the wave's next block
+                } else if (mode == kClaim) {
+                    const uint32_t qq = cl_next - min(avail, (uint32_t)__popcll(m)) + rank;
+                    {
+                        q = qq;
+                        uint32_t c0;
+                        if (!decode(q, c0)) {
+                            mode = kClaim;  // outside the image: nothing to render, claim again
+                        } else {
+                            uget(0) = q;
+                            n_cur = c0;
+                            acc[0 * kBlock] = 0.0, acc[1 * kBlock] = 0.0, acc[2 * kBlock] = 0.0;
+                            const double seed = seeds[(uint32_t)py * (uint32_t)W + (uint32_t)px];
+                            fgi = (float)(seed / (double)S.n_list);  // tracer.cl:840
+                            R().f[0] = fgi;
+                            R().f[1] = (float)(seed / (double)samples);  // fgi2, tracer.cl:841
+                            if (n_cur < c_end) {
+                                mode = kNeedCam;
+                            } else {  // an empty chunk (the range ends before it)
+                                double* o = part + (size_t)q * 4;
+                                o[0] = 0.0, o[1] = 0.0, o[2] = 0.0, o[3] = 0.0;
+                                uget(0) = kSlotFree;
+                                mode = kClaim;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        // C. Camera rays for the lanes starting a sample (batched: the camera block runs for
+        //    many lanes at once, as in the mesh kernel's refills).
+        {
+            const int n_cam = __popcll(__ballot(mode == kNeedCam));
+            if (n_cam && (n_cam >= PTMI_SPLIT_BATCH || !__any(tr))) {
+                n_yield += (uint32_t)__popcll(__ballot(mode == kNeedCam && spent >= B.budget));
+                if (mode == kNeedCam && spent >= B.budget) {  // yield: the next pass goes on from n_cur
+                    uget(1) = n_cur;
+                    uget(2) = kFlagYield;
+                    dget(12) = acc[0 * kBlock], dget(13) = acc[1 * kBlock], dget(14) = acc[2 * kBlock];
+                    mode = kNoSlot;
+                }
+                if (mode == kNeedCam) {
+                    spent++;
+                    const float fgi2 = R().f[1];
+                    float rx, ry;
+                    camera_offsets<FL>(fgi, fgi2, 0, n_cur, rx, ry);
+                    d4 ro, rd;
+                    ray_for_pixel<kDof, A>(S.cam, sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n_cur, ro, rd);
+                    start_path<A, kDof>(P, ro, rd);
+                    mode = kTrace;
+                }
+            }
+        }
+        if (!__any(mode != kExhausted)) {
+            if (lane == 0) {
+                B.wcl[2 * blockIdx.x] = cl_next;
+                B.wcl[2 * blockIdx.x + 1] = cl_end;
+                B.seg[blockIdx.x] = n_req;
+                if (n_req) {
+                    atomicAdd(&B.cnt[0], n_req);
+                    atomicAdd(&B.cnt[3], n_req);  // all passes (diagnostics)
+                }
+                if (n_yield) atomicAdd(&B.cnt[2], n_yield);
+            }
+            break;
+        }
+        // D. Closest primitive; a ray whose segment can meet a mesh hull saves its path and
+        //    asks for a walk.
+        bool walk = false;
+        if (mode == kTrace) {
+            if (P.dead) {
+                h.pk = -1;
+                mode = kReady;
+            } else {
+                h = find_closest_prims<FL>(S, P.ro, P.rd);
+                if (group_needs_walk<A>(S, P.ro, P.rd, h)) {
+                    dget(0) = P.ro.x, dget(1) = P.ro.y, dget(2) = P.ro.z;
+                    dget(3) = P.rd.x, dget(4) = P.rd.y, dget(5) = P.rd.z;
+                    dget(6) = P.mr, dget(7) = P.mg, dget(8) = P.mb;
+                    dget(9) = P.ar, dget(10) = P.ag, dget(11) = P.ab;
+                    dget(12) = acc[0 * kBlock], dget(13) = acc[1 * kBlock], dget(14) = acc[2 * kBlock];
+                    dget(15) = h.t;
+                    uget(1) = n_cur;
+                    uget(2) = P.b | (P.effective << 4) | ((P.inside ? 1u : 0u) << 7) | ((P.done ? 1u : 0u) << 8);
+                    uget(3) = (uint32_t)h.pk;
+                    walk = true;
+                    mode = kNoSlot;
+                } else {
+                    mode = kReady;
+                }
+            }
+        }
+        {  // the walk requests of this step, appended to the wave's own segment
+            const uint64_t wm = __ballot(walk);
+            if (walk) B.req[base + n_req + (uint32_t)__popcll(wm & ((1ull << lane) - 1))] = slot;
+            n_req += (uint32_t)__popcll(wm);
+        }
+        // E. Shading (tracer.cl:886-1110); a finished path adds to the pixel-chunk's sums
+        //    (tracer.cl:1179), a finished chunk writes its record (r, g, b, samples).
+        if (mode == kReady) {
+            if (bounce_shade<FL>(S, P, h, fgi, n_cur)) {
+                acc[0 * kBlock] = acc[0 * kBlock] + P.ar;
+                acc[1 * kBlock] = acc[1 * kBlock] + P.ag;
+                acc[2 * kBlock] = acc[2 * kBlock] + P.ab;
+                n_cur++;
+                if (n_cur < c_end) {
+                    mode = kNeedCam;
+                } else {
+                    uint32_t c0;
+                    decode(q, c0);
+                    double* o = part + (size_t)q * 4;
+                    o[0] = acc[0 * kBlock], o[1] = acc[1 * kBlock], o[2] = acc[2 * kBlock];
+                    o[3] = (double)(c_end - c0);
+                    uget(0) = kSlotFree;
+                    mode = kClaim;
+                }
+            } else {
+                mode = kTrace;
+            }
+        }
+    }
+}
+
+// The walks of one split pass: every request appended by trace_split_kernel.
+__global__ __launch_bounds__(kBlock, PTMI_WALK_WAVES) void walk_split_kernel(DevScene S, SplitBufs B) {
+    __shared__ int stk_lds[kStack * kStkStride];
+    LdsInt* stk = lds_ptr(stk_lds + threadIdx.x);
+    const uint32_t nseg = (B.L + B.per_wave - 1) / B.per_wave;
+    for (uint32_t w = blockIdx.x; w < nseg; w += gridDim.x)  // tracer wave w's segment
+        for (uint32_t i = threadIdx.x, n = B.seg[w]; i - threadIdx.x < n; i += kBlock) {
+            if (i >= n) continue;
+            const uint32_t slot = B.req[(size_t)w * B.per_wave + i];
+            SplitRec& Rs = reinterpret_cast<SplitRec*>(B.rec)[slot];
+            const double* d = Rs.d;
+            Hit h{d[15], (int)Rs.u[3], -1, -1, 0.0, 0.0};
+            group_walks<true>(S, stk, mk(d[0], d[1], d[2], 1.0), mk(d[3], d[4], d[5], 0.0), h);
+            Rs.res = WalkRes{h.t, h.pk, h.tri, h.ti, 0, h.u, h.v};
+        }
+}
+
+bool split_supported(int flags) {
+    return (flags & F_GROUPS) && !(flags & (F_PROJ | F_TEX | F_XRNG));
+}
+
+const void* trace_split_symbol(int flags) {
+    switch (flags & F_ALL) {
+#define K(f) \
+    case f: return reinterpret_cast<const void*>(&trace_split_kernel<f>);
+        K(1) K(3) K(5) K(7) K(9) K(11) K(13) K(15)
+#undef K
+    }
+    return nullptr;
+}
+const void* walk_split_symbol() { return reinterpret_cast<const void*>(&walk_split_kernel); }
+
+hipError_t launch_split_pass(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const SplitBufs& B,
+                             const double* seeds, const double* sunf, double* part, uint32_t walk_grid,
+                             hipStream_t st) {
+    if (!split_supported(flags)) return hipErrorInvalidValue;
+    const dim3 grid((B.L + B.per_wave - 1) / B.per_wave), block(kBlock);
+    switch (flags & F_ALL) {
+#define K(f)                                                                                                   \
+    case f:                                                                                                    \
+        hipLaunchKernelGGL(trace_split_kernel<f>, grid, block, 0, st, S, samples, WP, B, seeds, sunf, part); \
+        break;
+        K(1) K(3) K(5) K(7) K(9) K(11) K(13) K(15)
+#undef K
+    default:
+        return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(walk_split_kernel, dim3(walk_grid), block, 0, st, S, B);
+    return hipGetLastError();
+}
+
 hipError_t launch_walk(const DevScene& S, int flags, int mode, const WalkReq* req, uint32_t n, WalkRes* res,
                        uint32_t* next, uint32_t grid, hipStream_t st) {
     if (n == 0) return hipSuccess;

@@ -261,6 +261,19 @@ class Scene:
         err = ctypes.create_string_buffer(256)
         _check(self._lib.ptmi_scene_set_rng(self._h, int(mode), err, len(err)), err)
 
+    def set_split(self, enable=True):
+        """Diagnostics (include/ptmi_diag.h): mesh scenes in the split form or the (default)
+        one-kernel form.  Returns False when the library lacks the switch."""
+        if not hasattr(self._lib, "ptmi_diag_set_split"):
+            return False
+        self._lib.ptmi_diag_set_split.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        return self._lib.ptmi_diag_set_split(self._h, 1 if enable else 0) == 0
+
+    def split_passes(self):
+        self._lib.ptmi_diag_split_passes.restype = ctypes.c_int
+        self._lib.ptmi_diag_split_passes.argtypes = [ctypes.c_void_p]
+        return self._lib.ptmi_diag_split_passes(self._h)
+
     def set_timing(self, enable=True):
         self._lib.ptmi_scene_set_timing(self._h, 1 if enable else 0)
 
