@@ -51,7 +51,7 @@ using namespace ptmi;
 struct ptmi_scene {
     int device = 0;
     DevScene dev{};
-    void* buffers[14] = {};  // [10..12]: texture arrays, [13]: hemisphere table
+    void* buffers[15] = {};  // [10..12]: texture arrays, [13]: hemisphere table, [14]: camera record
     double* partial = nullptr;  // chunk partial sums, grown on demand
     double* sunf = nullptr;     // DoF aperture table for sunf_samples (sunflower_kernel)
     uint32_t sunf_samples = 0;
@@ -521,6 +521,11 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     if (const char* t = getenv("PTMI_SPLIT_BUDGET")) s->split_budget = (uint32_t)std::max(1, atoi(t));
     s->dev.n_tri = hs.n_tri;
     s->dev.cam = hs.cam;
+    {  // the camera record in device memory (ptmi_kernels.hip camera_ptr)
+        SCENE_TRY(hipMalloc(&s->buffers[14], sizeof(DevCamera)));
+        SCENE_TRY(hipMemcpy(s->buffers[14], &hs.cam, sizeof(DevCamera), hipMemcpyHostToDevice));
+        s->dev.camg = (const DevCamera*)s->buffers[14];
+    }
     SCENE_TRY(resident_waves(s));
 #undef SCENE_TRY
     *out = s;

@@ -162,6 +162,7 @@ struct DevScene {
     uint32_t n_nodes, n_tri;
     uint32_t n_list;  // numObjects of the reference's list (fgi = seed / numObjects, tracer.cl:840)
     DevCamera cam;
+    const DevCamera* camg;  // the same record in device memory (camera_ptr: reloaded where used)
     DevTexArray tex[3];  // textures, sphereTextures, cubeMapTextures (tracer.cl:833)
     const double* hemi;  // randomVectorInHemisphere table, 2^16 x 4 doubles (hemi_table_kernel)
 };

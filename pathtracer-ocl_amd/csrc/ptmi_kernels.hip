@@ -1347,6 +1347,21 @@ __device__ __noinline__ void sunflower(int amount, int point, double& ox, double
     oy = r * st;
 }
 
+// The camera record through a pointer the compiler cannot follow across loop iterations:
+// its fields are scalar-loaded where a camera block runs, instead of being held in SGPRs
+// through the whole bounce loop -- which spilled them into VGPR lanes (v_writelane /
+// v_readlane, VALU instructions) when the loop's other uniform values needed the SGPRs.
+#ifndef PTMI_CAM_RELOAD
+#define PTMI_CAM_RELOAD 1  // 1: kernels without meshes, 2: mesh kernels, 3: both
+#endif
+template <bool kReload = true>
+__device__ __forceinline__ const DevCamera& camera_ptr(const DevScene& S) {
+    if constexpr (!kReload) return S.cam;
+    const DevCamera* p = S.camg;
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+
 // rayForPixel (tracer.cl:745-779).  With DoF the aperture offset
 // sunflower(S, 2, n) depends only on n: it is read from a per-frame table
 // (sunflower_kernel) made with the same arithmetic.
@@ -1850,11 +1865,12 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
         const int n_need = __popcll(__ballot(need));
         const int n_starve = __popcll(__ballot(!buffered && !active && n_gen < c_end));
         if (n_need >= kRefillNeed || n_starve >= PTMI_REFILL_STARVE_GROUPS || (n_starve > 0 && !__any(active))) {
+            const DevCamera& cam = camera_ptr<(PTMI_CAM_RELOAD & 2) != 0>(S);
             if (need) {
                 d4 ro, rd;
                 float rx, ry;
                 camera_offsets<FL>(fgi, fgi2, seed_bits, n_gen, rx, ry);
-                ray_for_pixel<kDof, A>(S.cam, sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n_gen, ro, rd);
+                ray_for_pixel<kDof, A>(cam, sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n_gen, ro, rd);
                 double* cb = cam_lds + tid;
                 cb[0 * kBlock] = rd.x;
                 cb[1 * kBlock] = rd.y;
@@ -1879,7 +1895,10 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
             if constexpr (kCamComp > 3)
                 cro = mk(cb[3 * kBlock], cb[4 * kBlock], cb[5 * kBlock], A ? 1.0 : cb[(kCamComp - 2) * kBlock]);
             else
-                cro = mk(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], 1.0);  // ray_for_pixel's origin
+                {
+                    const double* co = camera_ptr<(PTMI_CAM_RELOAD & 2) != 0>(S).origin;  // ray_for_pixel's origin
+                    cro = mk(co[0], co[1], co[2], 1.0);
+                }
             start_path<A, kDof>(P, cro, crd);
             n_cur = n_gen - 1;
             if constexpr ((FL & F_XRNG) != 0) P.rng = xseed(seed_bits, n_cur);
@@ -2013,11 +2032,12 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
             const int n_need = __popcll(__ballot(need));
             const int n_starve = __popcll(__ballot(!buffered && !active && n_gen < c_end));
             if (n_need >= kRefillNeed || n_starve >= PTMI_REFILL_STARVE || (n_starve > 0 && !__any(active))) {
+                const DevCamera& cam = camera_ptr<(PTMI_CAM_RELOAD & 1) != 0>(S);
                 if (need) {
                     d4 ro, rd;
                     float rx, ry;
                     camera_offsets<FL>(fgi, fgi2, seed_bits, n_gen, rx, ry);
-                    ray_for_pixel<(FL & F_DOF) != 0, A>(S.cam, sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n_gen,
+                    ray_for_pixel<(FL & F_DOF) != 0, A>(cam, sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n_gen,
                                                         ro, rd);
                     double* cbuf = cam_lds + tid;
                     cbuf[0 * kWg] = rd.x;
@@ -2043,7 +2063,10 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
                 if constexpr (kCamComp > 3)
                     cro = mk(cbuf[3 * kWg], cbuf[4 * kWg], cbuf[5 * kWg], A ? 1.0 : cbuf[(kCamComp - 2) * kWg]);
                 else
-                    cro = mk(S.cam.origin[0], S.cam.origin[1], S.cam.origin[2], 1.0);  // ray_for_pixel's origin
+                    {
+                    const double* co = camera_ptr<(PTMI_CAM_RELOAD & 1) != 0>(S).origin;  // ray_for_pixel's origin
+                    cro = mk(co[0], co[1], co[2], 1.0);
+                }
                 start_path<A, (FL & F_DOF) != 0>(P, cro, crd);
                 acm[0 * kBlock] = 0.0;
                 acm[1 * kBlock] = 0.0;
@@ -2416,7 +2439,7 @@ __global__ __launch_bounds__(kBlock, PTMI_WAVES_SPLIT) void trace_split_kernel(D
                     float rx, ry;
                     camera_offsets<FL>(fgi, fgi2, 0, n_cur, rx, ry);
                     d4 ro, rd;
-                    ray_for_pixel<kDof, A>(S.cam, sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n_cur, ro, rd);
+                    ray_for_pixel<kDof, A>(camera_ptr(S), sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n_cur, ro, rd);
                     start_path<A, kDof>(P, ro, rd);
                     mode = kTrace;
                 }
