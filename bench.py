@@ -216,6 +216,8 @@ def main():
                     help="other configs timed after the headline at the same GPU count: a comma list, none, or "
                          "auto (c3,c5 after a default c2 run at full spp)")
     ap.add_argument("--extra-steps", type=int, default=2)
+    ap.add_argument("--rng", default="noise3d", choices=("noise3d", "xoshiro"),
+                    help="xoshiro: the headline config in the opt-in statistical RNG mode (profiling; not `value`)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -428,7 +430,8 @@ def main():
         return roof
 
     res, (objs, tris, grps, cam, S, seeds_host) = run_config(args.config, args.steps, args.warmup, args.samples,
-                                                             args.chunks, args.save_image)
+                                                             args.chunks, args.save_image,
+                                                             rng=api.RNG_XOSHIRO if args.rng == "xoshiro" else 0)
     # The other BASELINE configurations at this GPU count, after the headline frames
     # (C3 / C5 are the reference's 8-GPU configurations; the driver's 1/2/4/8 runs then
     # measure their scaling too).  Secondary: `value` and `ms_per_step` are the headline's.
