@@ -193,7 +193,7 @@ int ptmi_fill_seeds(double* seeds_dev, uint32_t n, uint64_t seed_stream, void* h
  * reference's noise3D hash (tracer.cl:314-317, called at :869, 982, 993, 1014, 1038,
  * 1057), bit for bit: images equal the reference kernel's.  PTMI_RNG_XOSHIRO is an
  * opt-in STATISTICAL mode: the same uniforms drawn from xoshiro128**, one stream per
- * (pixel, sample) path seeded from the pixel's seed and the sample index (SplitMix64),
+ * (pixel, sample) path seeded from the pixel's seed and the sample index (32-bit hash),
  * so images are deterministic and independent of the work split, and converge to the
  * same expectation as the parity mode, but do not equal the reference's.  Affine,
  * untextured scenes only (else PTMI_ERR_UNSUPPORTED). */
@@ -215,7 +215,8 @@ const char* ptmi_build_info(void);
  *   [0] Node4 count  [1] occupied child slots  [2] sum over occupied slots of the
  *   decoded child box's surface area, in object-space units  [3] infinite bounds among
  *   them  [4] largest root scale exponent s (bounds stored as (b - ctr) / 2^s)
- *   [5] roots.  Index quality (box inflation from the binary16 bounds) can be compared
+ *   [5] roots  [6] longest chain of Node4s (the walk's stack holds <= 3 entries per
+ *   level; ptmi_bvh.cpp keeps it <= 7).  Index quality (box inflation from the binary16 bounds) can be compared
  *   across translated or scaled copies of one mesh. */
 int ptmi_index_stats(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
                      const void* groups, uint32_t n_grp, const void* camera, double* out, int n_out,

@@ -654,17 +654,19 @@ int ptmi_index_stats(const void* objects, uint32_t n_obj, const void* triangles,
     HostScene hs;
     int rc = prepare_scene(objects, n_obj, triangles, n_tri, groups, n_grp, camera, nullptr, hs, err, err_len);
     if (rc) return rc;
-    double st[6] = {(double)hs.index.nodes.size(), 0.0, 0.0, 0.0, 0.0, (double)hs.root_rec.size()};
+    double st[7] = {(double)hs.index.nodes.size(), 0.0, 0.0, 0.0, 0.0, (double)hs.root_rec.size(), 0.0};
     for (const RootRec& R : hs.root_rec) {
         st[4] = std::max(st[4], std::log2((double)R.sc));
-        std::vector<int32_t> todo;
-        if (R.entry >= 0) todo.push_back(R.entry);
+        std::vector<std::pair<int32_t, int>> todo;  // (Node4, its level)
+        if (R.entry >= 0) todo.push_back({R.entry, 1});
         while (!todo.empty()) {  // the root's Node4s (children >= 0 are Node4 indices)
-            const Node4& nd = hs.index.nodes[todo.back()];
+            const auto [ni, lv] = todo.back();
+            const Node4& nd = hs.index.nodes[ni];
             todo.pop_back();
+            st[6] = std::max(st[6], (double)lv);
             for (int i = 0; i < 4; i++) {
                 if (nd.child[i] == kEmptyChild) continue;
-                if (nd.child[i] >= 0) todo.push_back(nd.child[i]);
+                if (nd.child[i] >= 0) todo.push_back({nd.child[i], lv + 1});
                 double e[3];
                 for (int k = 0; k < 3; k++) {
                     const double lo = f16_value(nd.bnd[k][0][i]), hi = f16_value(nd.bnd[k][1][i]);
@@ -676,7 +678,7 @@ int ptmi_index_stats(const void* objects, uint32_t n_obj, const void* triangles,
             }
         }
     }
-    for (int i = 0; i < n_out && i < 6; i++) out[i] = st[i];
+    for (int i = 0; i < n_out && i < 7; i++) out[i] = st[i];
     return PTMI_OK;
 }
 

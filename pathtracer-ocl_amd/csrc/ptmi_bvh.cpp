@@ -48,7 +48,8 @@ struct BNode {  // binary build node
 };
 
 constexpr int kLeafMax = 7;         // 3-bit count in the leaf entry code
-constexpr int kMaxBinaryDepth = 14; // BVH4 depth <= 7: 3 pushes per level fit kStack = 24
+constexpr int kMaxBinaryDepth = 14; // binary leaves at depth <= 14, so BVH4 chains of <= 7 nodes
+constexpr int kMaxNode4Depth = 7;   // 3 pushes per Node4 level: the kernel's stack needs 21 entries
 constexpr int kBins = 32;
 
 double area(const double* mn, const double* mx) {
@@ -348,16 +349,25 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
     // inner children), emitted breadth first: the top levels of the first
     // object's index are the first Node4s, which the kernel stages in LDS.
     std::vector<std::pair<int, int>> work;  // (binary node, Node4 slot), a FIFO
+    std::vector<int> level;                 // 1-based Node4 level of work[i]
     size_t work_head = 0;
+    int cur_level = 0;
     auto emit = [&](int bi) -> int32_t {
         if (B.nodes[bi].left < 0) return code_of(bi);
         const int32_t slot = (int32_t)out.nodes.size();
         out.nodes.emplace_back();
         work.push_back({bi, slot});
+        level.push_back(cur_level + 1);
         return slot;
     };
     *entry = emit(broot);
     while (work_head < work.size()) {
+        cur_level = level[work_head];
+        // The kernel's traversal stack holds 3 entries per Node4 level (kStack >= 21).
+        if (cur_level > kMaxNode4Depth) {
+            std::snprintf(err, err_len, "BVH4 of root %d deeper than %d levels", root, kMaxNode4Depth);
+            return PTMI_ERR_UNSUPPORTED;
+        }
         auto [bi, slot] = work[work_head++];
         int kids[4], nk = 0;
         for (int c : {B.nodes[bi].left, B.nodes[bi].right}) {

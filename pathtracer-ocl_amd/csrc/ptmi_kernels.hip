@@ -280,10 +280,10 @@ __device__ __forceinline__ float noise3d(float x, float y, float z) {
 // The reference's noise3D (above) is a hash of (seed, sample, bounce) through a float
 // sin with large-argument reductions -- the parity path keeps it bit for bit.  The
 // statistical mode draws the same uniforms from xoshiro128** (Blackman & Vigna): one
-// stream per path, seeded from the pixel's seed bits and the sample index through
-// SplitMix64, so the image does not depend on which lane, chunk or GPU traces a
-// sample; the camera's two anti-aliasing offsets come from a separate SplitMix64 draw
-// of the same pair.  Uniform floats are the top 24 bits x 2^-24, in [0, 1) like fract.
+// stream per path, seeded from the pixel's seed bits and the sample index through a
+// 32-bit hash (xseed), so the image does not depend on which lane, chunk or GPU traces
+// a sample; the camera's two anti-aliasing offsets come from two more hashes of the
+// same pair.  Uniform floats are the top 24 bits x 2^-24, in [0, 1) like fract.
 struct Xrng {
     uint32_t s0, s1, s2, s3;
 };
@@ -318,18 +318,54 @@ __device__ __forceinline__ float xnext16(Xrng& r) {
     r.s3 = rotl32(r.s3, 11);
     return (float)(res >> 16) * 0x1p-16f;
 }
-__device__ __forceinline__ Xrng xseed(uint64_t seed_bits, uint32_t n) {
+#ifndef PTMI_XSEED32
+#define PTMI_XSEED32 1
+#endif
+// 32-bit integer finaliser (lowbias32 form: two 32-bit multiplies, three xor-shifts).
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
+#if PTMI_XSEED32
+// The pixel's stream key: its seed's 64 bits folded once per work item (xseed_of), so a
+// path seeds from (key, n) with 32-bit multiplies only: xoshiro128**'s four state words
+// are four independent finalisations of (key, n), eight 32-bit multiplies per path (round
+// 3 took two SplitMix64 draws, four 64-bit multiplies, and a third for the camera).
+typedef uint32_t XSeed;
+__device__ __forceinline__ XSeed xseed_of(uint64_t seed_bits) {
+    return mix32((uint32_t)seed_bits ^ mix32((uint32_t)(seed_bits >> 32) + 0x9E3779B9u));
+}
+__device__ __forceinline__ Xrng xseed(XSeed key, uint32_t n) {
+    const uint32_t x = key ^ (n * 0x9E3779B9u);
+    Xrng r{mix32(x + 0x632BE5ABu), mix32(x + 0x85157AF5u), mix32(x + 0x2545F491u), mix32(x + 0xB5297A4Du)};
+    if ((r.s0 | r.s1 | r.s2 | r.s3) == 0) r.s0 = 1;  // the all-zero state is the one fixed point
+    return r;
+}
+__device__ __forceinline__ void xcamera(XSeed key, uint32_t n, float& rx, float& ry) {
+    const uint32_t x = key ^ (n * 0x9E3779B9u);
+    rx = (float)(mix32(x + 0x68E31DA4u) >> 8) * 0x1p-24f;
+    ry = (float)(mix32(x + 0x1B56C4E9u) >> 8) * 0x1p-24f;
+}
+#else
+typedef uint64_t XSeed;
+__device__ __forceinline__ XSeed xseed_of(uint64_t seed_bits) { return seed_bits; }
+__device__ __forceinline__ Xrng xseed(XSeed seed_bits, uint32_t n) {
     const uint64_t base = seed_bits ^ (0x9E3779B97F4A7C15ull * ((uint64_t)n + 1));
     const uint64_t a = splitmix64(base + 0x9E3779B97F4A7C15ull), b = splitmix64(base + 0x3C6EF372FE94F82Aull);
     Xrng r{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
     if ((r.s0 | r.s1 | r.s2 | r.s3) == 0) r.s0 = 1;  // the all-zero state is the one fixed point
     return r;
 }
-__device__ __forceinline__ void xcamera(uint64_t seed_bits, uint32_t n, float& rx, float& ry) {
+__device__ __forceinline__ void xcamera(XSeed seed_bits, uint32_t n, float& rx, float& ry) {
     const uint64_t v = splitmix64(seed_bits + 0xD1B54A32D192ED03ull * ((uint64_t)n + 1));
     rx = (float)(uint32_t)(v >> 40) * 0x1p-24f;
     ry = (float)(uint32_t)((v >> 16) & 0xFFFFFFu) * 0x1p-24f;
 }
+#endif
 // checkAxis (tracer.cl:250-268)
 __device__ __forceinline__ void check_axis(double o, double d, double mn, double mx, double& t0, double& t1) {
     double a0 = mn - o, a1 = mx - o;
@@ -412,7 +448,7 @@ enum : int {
 
 // The camera ray's two anti-aliasing offsets of sample n (tracer.cl:869).
 template <int FL>
-__device__ __forceinline__ void camera_offsets(float fgi, float fgi2, uint64_t seed_bits, uint32_t n, float& rx,
+__device__ __forceinline__ void camera_offsets(float fgi, float fgi2, XSeed seed_bits, uint32_t n, float& rx,
                                                float& ry) {
     if constexpr ((FL & F_XRNG) != 0) {
         xcamera(seed_bits, n, rx, ry);
@@ -580,7 +616,16 @@ __device__ __forceinline__ void tri_uv(const DevTri& T, d4 o, d4 d, double& u, d
     v = f * dv;
 }
 
-static constexpr int kStack = 24;  // per-lane LDS traversal stack (3 pushes x BVH4 depth <= 7, ptmi_bvh.cpp)
+#ifndef PTMI_STACK
+#define PTMI_STACK 24
+#endif
+#ifndef PTMI_GROUP_ACM
+#define PTMI_GROUP_ACM 0
+#endif
+// Per-lane LDS traversal stack: a Node4 visit pushes <= 3 entries and BVH4 chains are <= 7
+// nodes long (ptmi_bvh.cpp checks it), so a walk holds <= 21 entries.
+static constexpr int kStack = PTMI_STACK;
+static_assert(kStack >= 21, "the BVH4 depth bound of ptmi_bvh.cpp needs 21 stack entries");
 // The traversal stack's pointer type: LDS (address space 3), so every push and pop is a
 // ds_write / ds_read whatever the optimiser makes of the pointer (a loop-carried generic
 // pointer had turned the pop into a flat load).
@@ -1832,6 +1877,11 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
     // registers are what the walk phases need.
     __shared__ int stk_lds[kStack * kStkStride];
     __shared__ double acc_lds[3 * kBlock];
+    // accumColor of the lane's current path in LDS (bounce_shade kAccLds), as in the kernels
+    // without meshes: it changes only on bounces that see emission, and in registers the
+    // 4-wave budget spilled it with a load and a store per bounce.
+    constexpr bool kAcm = PTMI_GROUP_ACM != 0;
+    __shared__ double acm_lds[kAcm ? 3 * kBlock : 1];
     __shared__ double hp_t_lds[kBlock];
     __shared__ int hp_pk_lds[kBlock];
     __shared__ double cam_lds[kCamComp * kBlock];
@@ -1846,13 +1896,14 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
     const double seed = it.inside ? seeds[it.i] : 0.0;
     const float fgi = (float)(seed / (double)S.n_list);
     const float fgi2 = (float)(seed / (double)samples);
-    const uint64_t seed_bits = (uint64_t)__double_as_longlong(seed);
+    const XSeed seed_bits = xseed_of((uint64_t)__double_as_longlong(seed));  // statistical mode
     const uint32_t c_end = it.inside ? it.c1 : it.c0;
     LdsInt* stk = lds_ptr(stk_lds + tid);
     double* acc = acc_lds + tid;
     acc[0 * kBlock] = 0.0;
     acc[1 * kBlock] = 0.0;
     acc[2 * kBlock] = 0.0;
+    double* acm = kAcm ? acm_lds + tid : nullptr;
     uint32_t n_gen = it.c0, n_cur = 0;
     bool buffered = false, active = false, pending = false;
     PathState P;
@@ -1900,6 +1951,11 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
                     cro = mk(co[0], co[1], co[2], 1.0);
                 }
             start_path<A, kDof>(P, cro, crd);
+            if constexpr (kAcm) {
+                acm[0 * kBlock] = 0.0;
+                acm[1 * kBlock] = 0.0;
+                acm[2 * kBlock] = 0.0;
+            }
             n_cur = n_gen - 1;
             if constexpr ((FL & F_XRNG) != 0) P.rng = xseed(seed_bits, n_cur);
             buffered = false;
@@ -1950,10 +2006,16 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
         }
         PTMI_TADD(14, t_c);
         PTMI_TSTAMP(t_d);
-        if (ready && bounce_shade<FL>(S, P, h, fgi, n_cur)) {
-            acc[0 * kBlock] = acc[0 * kBlock] + P.ar;  // colors += accumColor (tracer.cl:1179)
-            acc[1 * kBlock] = acc[1 * kBlock] + P.ag;
-            acc[2 * kBlock] = acc[2 * kBlock] + P.ab;
+        if (ready && bounce_shade<FL, kAcm>(S, P, h, fgi, n_cur, acm)) {
+            if constexpr (kAcm) {
+                acc[0 * kBlock] = acc[0 * kBlock] + acm[0 * kBlock];  // colors += accumColor (tracer.cl:1179)
+                acc[1 * kBlock] = acc[1 * kBlock] + acm[1 * kBlock];
+                acc[2 * kBlock] = acc[2 * kBlock] + acm[2 * kBlock];
+            } else {
+                acc[0 * kBlock] = acc[0 * kBlock] + P.ar;
+                acc[1 * kBlock] = acc[1 * kBlock] + P.ag;
+                acc[2 * kBlock] = acc[2 * kBlock] + P.ab;
+            }
             active = false;
         }
         PTMI_TADD(15, t_d);
@@ -1995,7 +2057,7 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
         const double seed = it.inside ? seeds[it.i] : 0.0;
         const float fgi = (float)(seed / (double)S.n_list);
         const float fgi2 = (float)(seed / (double)samples);
-        const uint64_t seed_bits = (uint64_t)__double_as_longlong(seed);
+        const XSeed seed_bits = xseed_of((uint64_t)__double_as_longlong(seed));  // statistical mode
         const uint32_t c_end = it.inside ? it.c1 : it.c0;
         // colors (tracer.cl:1179): one LDS slot per lane, the same additions in the same
         // order; they change once per path, and the registers keep the bounce loop off

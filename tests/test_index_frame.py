@@ -51,3 +51,17 @@ def test_large_mesh_gets_finite_scaled_bounds(teapot, scale, offset):
     st = _stats(*moved(objs, tris, grps, offset=offset, scale=scale), cam)
     assert st["inf_bounds"] == 0 and st["max_scale_exp"] > 0, st
     assert abs(st["box_area"] / (base["box_area"] * scale * scale) - 1.0) < 0.02, (st, base)
+
+
+@pytest.mark.parametrize("scene", ["teapot", "gopher", "adv:flat", "adv:stairs", "adv:dupes", "adv:far"])
+def test_node4_chains_fit_the_walk_stack(scene):
+    """The walk's LDS stack holds 3 entries per Node4 level (kStack >= 21 in
+    ptmi_kernels.hip): every index the builder emits has chains of <= 7 Node4s, on the
+    bench meshes and on the adversarial ones (tests/adversarial.py)."""
+    if scene.startswith("adv:"):
+        from tests import adversarial
+        objs, tris, grps, cam = adversarial.scene_inputs(scene[4:], 32, 24, 0.0, 0.0)
+    else:
+        objs, tris, grps, cam = scene_inputs(scene, 64, 48)
+    st = _stats(objs, tris, grps, cam)
+    assert 1 <= st["depth"] <= 7, st
