@@ -19,6 +19,11 @@ extern "C" {
 int ptmi_diag_capture_setup(void* req_dev, void* res_dev, uint32_t cap, char* err, size_t err_len);
 int ptmi_diag_capture_count(uint32_t* n, char* err, size_t err_len);
 
+/* Timeline builds only (make -C pathtracer-ocl_amd timeline -> build/libptmi_timeline.so):
+ * trace_kernel writes work item b's start and end wall-clock ticks (wall_clock64, 100 MHz)
+ * to buf_dev[2b], buf_dev[2b + 1] for b < cap.  Other builds return PTMI_ERR_UNSUPPORTED. */
+int ptmi_diag_timeline_setup(void* buf_dev, uint32_t cap, char* err, size_t err_len);
+
 /* Walk n requests of scene s with a standalone kernel, results to res_dev; *ms = its
  * time (HIP events on hip_stream).  mode 0: one request per lane (walk_kernel); mode 1:
  * persistent waves with per-lane refill from *counter_dev (walk_pool_kernel). */

@@ -60,6 +60,7 @@ struct ptmi_scene {
     uint32_t tail_tiles = 0;  // chunked tiles at the end of an automatic launch; 0: default (see render)
     uint32_t tail_items = 6;  // chunk items per resident wave slot in the tail (scenes without meshes; see render)
     uint32_t mesh_items = 32;  // chunk items per resident wave slot, mesh scenes (every tile chunked)
+    uint32_t min_chunk = 32;   // fewest samples per chunk item (see render)
     uint32_t width = 0, height = 0;
     int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
     int hemi_mismatch = 0;  // hemisphere-table records where affine and generic sequences differ (upload_scene)
@@ -514,6 +515,7 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     if (const char* t = getenv("PTMI_TAIL_TILES")) s->tail_tiles = (uint32_t)atoi(t);  // testing: small frames with whole tiles
     if (const char* t = getenv("PTMI_TAIL_ITEMS")) s->tail_items = (uint32_t)std::max(1, atoi(t));  // tuning
     if (const char* t = getenv("PTMI_MESH_ITEMS")) s->mesh_items = (uint32_t)std::max(1, atoi(t));  // tuning
+    if (const char* t = getenv("PTMI_MIN_CHUNK")) s->min_chunk = (uint32_t)std::max(1, atoi(t));    // tuning
     if (const char* t = getenv("PTMI_SPLIT")) s->split = atoi(t) != 0;
     if (const char* t = getenv("PTMI_SPLIT_CHUNK")) s->split_chunk = (uint32_t)std::max(1, atoi(t));
     if (const char* t = getenv("PTMI_SPLIT_SLOTS")) s->split_per_lane = (uint32_t)std::max(1, atoi(t));
@@ -786,7 +788,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
             n_tail = std::min<uint32_t>(owned_tiles, s->tail_tiles ? s->tail_tiles : (uint32_t)(s->resident_waves / 2));
         const uint64_t want = (uint64_t)s->resident_waves * (mesh ? s->mesh_items : s->tail_items);
         chunks = (uint32_t)std::min<uint64_t>((want + n_tail - 1) / std::max<uint32_t>(n_tail, 1),
-                                              std::max<uint32_t>(range / 32, 1));
+                                              std::max<uint32_t>(range / s->min_chunk, 1));
     }
     chunks = std::max<uint32_t>(1, std::min<uint32_t>(chunks, std::max<uint32_t>(range, 1)));
     const uint32_t chunk_len = range == 0 ? 1 : (range + chunks - 1) / chunks;
@@ -1162,7 +1164,18 @@ hipError_t launch_walk(const DevScene& S, int flags, int mode, const WalkReq* re
 const void* walk_kernel_symbol(int mode);
 hipError_t capture_setup(WalkReq* req, WalkRes* res, uint32_t cap);
 hipError_t capture_count(uint32_t* n);
+hipError_t timeline_setup(unsigned long long* buf, uint32_t cap);
 }  // namespace ptmi
+
+extern "C" int ptmi_diag_timeline_setup(void* buf_dev, uint32_t cap, char* err, size_t err_len) {
+    const hipError_t e = timeline_setup((unsigned long long*)buf_dev, cap);
+    if (e == hipErrorNotSupported) {
+        set_err(err, err_len, "not a timeline build (make -C pathtracer-ocl_amd timeline)");
+        return PTMI_ERR_UNSUPPORTED;
+    }
+    HIP_TRY(e);
+    return PTMI_OK;
+}
 
 extern "C" int ptmi_diag_capture_setup(void* req_dev, void* res_dev, uint32_t cap, char* err, size_t err_len) {
     const hipError_t e = capture_setup((WalkReq*)req_dev, (WalkRes*)res_dev, cap);

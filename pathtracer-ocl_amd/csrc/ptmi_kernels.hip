@@ -75,8 +75,20 @@ __shared__ unsigned long long ptmi_wstat[1][32];
 #ifndef PTMI_CAPTURE
 #define PTMI_CAPTURE 0
 #endif
+// PTMI_TIMELINE: DIAGNOSTIC build (make timeline) -- trace_kernel records each work
+// item's start and end (wall_clock64, lane 0, vector stores) into a device buffer set by
+// ptmi_diag_timeline_setup, for the launch's ramp / tail analysis (tools/timeline.py).
+// Same images; the product has PTMI_TIMELINE == 0.
+#ifndef PTMI_TIMELINE
+#define PTMI_TIMELINE 0
+#endif
 
 namespace ptmi {
+
+#if PTMI_TIMELINE
+__device__ unsigned long long* ptmi_tl;
+__device__ unsigned ptmi_tl_max;
+#endif
 
 #if PTMI_CAPTURE
 __device__ WalkReq* ptmi_cap_req;
@@ -1392,19 +1404,30 @@ __device__ __noinline__ void sunflower(int amount, int point, double& ox, double
     oy = r * st;
 }
 
-// The camera record through a pointer the compiler cannot follow across loop iterations:
-// its fields are scalar-loaded where a camera block runs, instead of being held in SGPRs
-// through the whole bounce loop -- which spilled them into VGPR lanes (v_writelane /
-// v_readlane, VALU instructions) when the loop's other uniform values needed the SGPRs.
+// The camera record through a pointer the compiler does not hoist: its fields are
+// scalar-loaded where a camera block runs, instead of being held in SGPRs through the
+// whole bounce loop -- which spilled them into VGPR lanes (v_writelane / v_readlane, VALU
+// instructions) when the loop's other uniform values needed the SGPRs.  C2 / C3 154.85 /
+// 160.89 -> 154.46 / 157.35 ms, C4 (512 spp) 165.84 -> 165.15 ms (profiles/r4/cam_reload).
+// A *volatile* asm here made every later global load of the loop a vector load (the
+// uniform-load analysis treats it as a possible store): C2 264 ms.
 #ifndef PTMI_CAM_RELOAD
-#define PTMI_CAM_RELOAD 1  // 1: kernels without meshes, 2: mesh kernels, 3: both
+#define PTMI_CAM_RELOAD 3  // 1: kernels without meshes, 2: mesh kernels, 3: both
 #endif
 template <bool kReload = true>
 __device__ __forceinline__ const DevCamera& camera_ptr(const DevScene& S) {
     if constexpr (!kReload) return S.cam;
+    // The constant address space: scalar loads of an invariant record (through a generic
+    // pointer the loads were per-lane vector loads: C2 155 -> 264 ms).
+    // readfirstlane: a value divergence analysis knows to be uniform, so the loads are
+    // scalar (an inline-asm "s" result alone is not).
+    typedef const __attribute__((address_space(4))) DevCamera ConstCam;
     const DevCamera* p = S.camg;
-    asm volatile("" : "+s"(p));
-    return *p;
+    asm("" : "+s"(p));
+    const uint64_t a = (uint64_t)p;
+    const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32);
+    return *(const DevCamera*)(ConstCam*)u;
 }
 
 // rayForPixel (tracer.cl:745-779).  With DoF the aperture offset
@@ -2042,8 +2065,17 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
                                                                        : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, WorkPlan WP,
                                                     const double* __restrict__ seeds, const double* __restrict__ sunf,
                                                     double* __restrict__ sums, double* __restrict__ part) {
+#if PTMI_TIMELINE
+    const unsigned long long tl0 = wall_clock64();
+#endif
     if constexpr ((FL & F_GROUPS) != 0) {
         trace_groups<FL>(S, samples, WP, seeds, sunf, sums, part);
+#if PTMI_TIMELINE
+        if (threadIdx.x == 0 && blockIdx.x < ptmi_tl_max) {
+            ptmi_tl[2 * blockIdx.x] = tl0;
+            ptmi_tl[2 * blockIdx.x + 1] = wall_clock64();
+        }
+#endif
     } else {
         constexpr bool A = !(FL & F_PROJ);
         const int tid = threadIdx.x, lane = tid & 63;
@@ -2164,6 +2196,12 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
 #endif
         store_sums<true>(work_item(S, WP, blockIdx.x, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock],
                    acc[2 * kBlock]);  // the work item re-derived: fewer live VGPRs
+#if PTMI_TIMELINE
+        if (threadIdx.x == 0 && blockIdx.x < ptmi_tl_max) {
+            ptmi_tl[2 * blockIdx.x] = tl0;
+            ptmi_tl[2 * blockIdx.x + 1] = wall_clock64();
+        }
+#endif
     }
 }
 
@@ -2658,6 +2696,15 @@ hipError_t capture_count(uint32_t* n) { return hipMemcpyFromSymbol(n, HIP_SYMBOL
 #else
 hipError_t capture_setup(WalkReq*, WalkRes*, uint32_t) { return hipErrorNotSupported; }
 hipError_t capture_count(uint32_t*) { return hipErrorNotSupported; }
+#endif
+#if PTMI_TIMELINE
+hipError_t timeline_setup(unsigned long long* buf, uint32_t cap) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(ptmi_tl), &buf, sizeof(buf));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(ptmi_tl_max), &cap, sizeof(cap));
+    return e;
+}
+#else
+hipError_t timeline_setup(unsigned long long*, uint32_t) { return hipErrorNotSupported; }
 #endif
 
 // DoF aperture offsets sunflower(S, 2, n) for n in [0, S) (tracer.cl:221-248,
