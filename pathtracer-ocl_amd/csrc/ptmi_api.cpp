@@ -61,6 +61,13 @@ struct ptmi_scene {
     uint32_t tail_items = 6;  // chunk items per resident wave slot in the tail (scenes without meshes; see render)
     uint32_t mesh_items = 32;  // chunk items per resident wave slot, mesh scenes (every tile chunked)
     uint32_t min_chunk = 32;   // fewest samples per chunk item (see render)
+    // Mesh scenes: per-tile cost class (mesh_tile_cost) and the dispatch order built from it
+    // for the last (tile_stride, tile_offset) rendered (see render).
+    bool tile_order = true;
+    std::vector<uint8_t> tile_cost;
+    std::vector<uint32_t> order_host;
+    uint32_t* order_dev = nullptr;
+    uint32_t order_stride = 0, order_offset = 0, order_n = 0;
     uint32_t width = 0, height = 0;
     int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
     int hemi_mismatch = 0;  // hemisphere-table records where affine and generic sequences differ (upload_scene)
@@ -426,6 +433,55 @@ hipError_t resident_waves(ptmi_scene* s) {
     return hipSuccess;
 }
 
+// Mesh scenes: a cost class per 8x8 tile for the dispatch order of the chunked tiles --
+// how many of 9 primary rays (a 3x3 grid of pixel centres) pass the conservative hull
+// cull of some group object (group_needs_walk without the primitives' best).  Tiles whose
+// camera rays reach a mesh walk on every bounce; their chunks are the long items of a
+// launch (C4 at 2048 spp: 20 ms on average, up to 82 ms), and in raster order the last
+// round of chunks ends on them (a 43 ms drain, 6 % of the slot-time; tools/timeline.py).
+// Dispatching them first within each chunk round leaves short items for the end.  Only the
+// order of work items changes, never a pixel's sums or their order.  Plain host doubles: a
+// heuristic, not an exactness argument.
+std::vector<uint8_t> mesh_tile_cost(const HostScene& hs) {
+    const DevCamera& c = hs.cam;
+    const int tx = (c.width + 7) / 8, ty = (c.height + 7) / 8;
+    std::vector<uint8_t> cost((size_t)tx * ty, 0);
+    const double* m = c.inv;
+    for (int t = 0; t < tx * ty; t++) {
+        int hits = 0;
+        for (int q = 0; q < 9; q++) {
+            const double x = (t % tx) * 8 + 1 + 3 * (q % 3) + 0.5, y = (t / tx) * 8 + 1 + 3 * (q / 3) + 0.5;
+            const double a = c.half_width - c.pixel_size * x, b = c.half_height - c.pixel_size * y;
+            double d[3];
+            for (int r = 0; r < 3; r++) d[r] = m[4 * r] * a + m[4 * r + 1] * b - m[4 * r + 2] + m[4 * r + 3] - c.origin[r];
+            bool hit = false;
+            for (int j = hs.run_end[3]; j < hs.run_end[4] && !hit; j++) {
+                const DevObject& ob = hs.objs[j];
+                double o[3], v[3], inv_d[3];
+                for (int r = 0; r < 3; r++) {
+                    const double* mi = ob.inv + 4 * r;
+                    o[r] = mi[0] * c.origin[0] + mi[1] * c.origin[1] + mi[2] * c.origin[2] + mi[3];
+                    v[r] = mi[0] * d[0] + mi[1] * d[1] + mi[2] * d[2];
+                    inv_d[r] = 1.0 / v[r];
+                }
+                for (int ci = 0; ci < ob.child_count && !hit; ci++) {
+                    const RootRec& R = hs.root_rec[ob.child_base + ci];
+                    double tn = 0.0, tf = INFINITY;
+                    for (int r = 0; r < 3; r++) {
+                        const double t0 = (R.hull_mn[r] - o[r]) * inv_d[r], t1 = (R.hull_mx[r] - o[r]) * inv_d[r];
+                        tn = std::max(tn, std::min(t0, t1));
+                        tf = std::min(tf, std::max(t0, t1));
+                    }
+                    hit = tn <= tf;  // NaN slabs (ray in a hull face plane) count as misses: a heuristic
+                }
+            }
+            hits += hit ? 1 : 0;
+        }
+        cost[t] = (uint8_t)hits;
+    }
+    return cost;
+}
+
 int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* textures, ptmi_scene** out, char* err,
                  size_t err_len) {
     HIP_TRY(hipSetDevice(device_index));
@@ -516,6 +572,8 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     if (const char* t = getenv("PTMI_TAIL_ITEMS")) s->tail_items = (uint32_t)std::max(1, atoi(t));  // tuning
     if (const char* t = getenv("PTMI_MESH_ITEMS")) s->mesh_items = (uint32_t)std::max(1, atoi(t));  // tuning
     if (const char* t = getenv("PTMI_MIN_CHUNK")) s->min_chunk = (uint32_t)std::max(1, atoi(t));    // tuning
+    if (const char* t = getenv("PTMI_TILE_ORDER")) s->tile_order = atoi(t) != 0;                     // tuning
+    if (hs.flags & 1) s->tile_cost = mesh_tile_cost(hs);
     if (const char* t = getenv("PTMI_SPLIT")) s->split = atoi(t) != 0;
     if (const char* t = getenv("PTMI_SPLIT_CHUNK")) s->split_chunk = (uint32_t)std::max(1, atoi(t));
     if (const char* t = getenv("PTMI_SPLIT_SLOTS")) s->split_per_lane = (uint32_t)std::max(1, atoi(t));
@@ -717,6 +775,7 @@ void ptmi_scene_destroy(ptmi_scene* s) {
     if (s->sunf) (void)hipFree(s->sunf);
     if (s->split_mem) (void)hipFree(s->split_mem);
     if (s->split_host) (void)hipHostFree(s->split_host);
+    if (s->order_dev) (void)hipFree(s->order_dev);
     for (auto& e : s->events) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
@@ -798,6 +857,30 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     wp.n_tail = n_tail;
     wp.nchunks = chunks;
     wp.chunk_len = chunk_len;
+    wp.order = nullptr;
+    if (!split && s->tile_order && !s->tile_cost.empty() && wp.n_whole == 0 && n_tail > 0) {
+        // Mesh scenes: the chunked tiles' dispatch order, costliest class first (mesh_tile_cost),
+        // raster order within a class; rebuilt when the rank's tile ownership changes.
+        if (s->order_stride != tile_stride || s->order_offset != tile_offset || s->order_n != n_tail) {
+            HIP_TRY(hipStreamSynchronize(st));  // order_host may still feed an earlier copy
+            s->order_host.resize(n_tail);
+            for (uint32_t k = 0; k < n_tail; k++) s->order_host[k] = k;
+            std::stable_sort(s->order_host.begin(), s->order_host.end(), [&](uint32_t a, uint32_t b) {
+                return s->tile_cost[tile_offset + a * tile_stride] > s->tile_cost[tile_offset + b * tile_stride];
+            });
+            if (s->order_dev && s->order_n < n_tail) {
+                HIP_TRY(hipFree(s->order_dev));
+                s->order_dev = nullptr;
+            }
+            if (!s->order_dev) HIP_TRY(hipMalloc((void**)&s->order_dev, (size_t)n_tail * sizeof(uint32_t)));
+            HIP_TRY(hipMemcpyAsync(s->order_dev, s->order_host.data(), (size_t)n_tail * sizeof(uint32_t),
+                                   hipMemcpyHostToDevice, st));
+            s->order_stride = tile_stride;
+            s->order_offset = tile_offset;
+            s->order_n = n_tail;
+        }
+        wp.order = s->order_dev;
+    }
     if ((s->flags & 8) && s->dev.cam.aperture != 0 && s->sunf_samples != samples) {  // DoF table for this S
         if (s->sunf) {
             HIP_TRY(hipStreamSynchronize(st));

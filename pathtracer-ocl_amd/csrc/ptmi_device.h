@@ -232,6 +232,10 @@ struct WorkPlan {
     uint32_t tile_stride, tile_offset;
     uint32_t n_whole, n_tail;
     uint32_t nchunks, chunk_len;
+    // Optional dispatch order of the chunked tiles within each chunk round: item tt of a
+    // round runs chunked tile order[tt] (a permutation of [0, n_tail)); nullptr = identity.
+    // The tile keeps its own partial slot, so the sums and their order do not change.
+    const uint32_t* order;
 };
 
 }  // namespace ptmi

@@ -1833,8 +1833,9 @@ __device__ __forceinline__ Item work_item(const DevScene& S, const WorkPlan& WP,
     } else {
         it.whole = false;
         const uint32_t t = item - WP.n_whole;
-        const uint32_t c = t / max(WP.n_tail, 1u), tt = t - c * WP.n_tail;
+        const uint32_t c = t / max(WP.n_tail, 1u), tq = t - c * WP.n_tail;
         if (c >= WP.nchunks) return it;
+        const uint32_t tt = WP.order ? WP.order[tq] : tq;  // the round's tq-th tile in dispatch order
         k = WP.n_whole + tt;
         it.c0 = WP.s_begin + c * WP.chunk_len;
         it.c1 = min(WP.s_end, it.c0 + WP.chunk_len);

@@ -82,8 +82,14 @@ res = {"config": a.config, "workload": desc, "samples": [s0, s1], "frame_spp": S
        "last_start_ms": round(float(last_start), 3), "drain_ms": round(float(span - last_start), 3),
        "ramp_ms": round(float(edges[np.argmax(act >= 0.95 * plateau)]), 3),
        "lost_slot_fraction": round(float(1.0 - busy / (plateau * span)), 4),
-       "tail_below_90pct_ms": round(float(span - edges[np.nonzero(act >= 0.9 * plateau)[0].max()]), 3)}
-print(json.dumps(res))
+       "tail_below_90pct_ms": round(float(span - edges[np.nonzero(act >= 0.9 * plateau)[0].max()]), 3),
+       # items in flight at 200 instants, and the start / end of the items by kind (whole
+       # tile or chunk: the longest tenth of the items vs the rest)
+       "curve": [[round(float(edges[i]), 3), int(act[i])] for i in range(0, 1000, 5)],
+       "long_items": {"count": int((dur >= np.percentile(dur, 90)).sum()),
+                      "last_end_ms": round(float(en[dur >= np.percentile(dur, 90)].max()), 3),
+                      "last_start_ms": round(float(st[dur >= np.percentile(dur, 90)].max()), 3)}}
+print(json.dumps({k: v for k, v in res.items() if k != "curve"}))
 if a.out:
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
