@@ -27,6 +27,8 @@ namespace ptmi {
 hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const double* seeds,
                         const double* sunf, double* sums, double* part, hipStream_t st);
 hipError_t launch_sunflower(double* out, uint32_t samples, hipStream_t st);
+hipError_t launch_tile_order(unsigned long long* cost, uint32_t n_tail, uint32_t stride, uint32_t offset,
+                             uint32_t* order, hipStream_t st);
 hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, int W, int H, bool planes,
                          hipStream_t st);
 hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint32_t samples, hipStream_t st);
@@ -63,10 +65,11 @@ struct ptmi_scene {
     uint32_t min_chunk = 32;   // fewest samples per chunk item (see render)
     // Mesh scenes: per-tile cost class (mesh_tile_cost) and the dispatch order built from it
     // for the last (tile_stride, tile_offset) rendered (see render).
-    bool tile_order = true;
+    int tile_order = 2;  // 0: raster order, 1: static (hull-hit classes), 2: measured by the last launch
     std::vector<uint8_t> tile_cost;
     std::vector<uint32_t> order_host;
     uint32_t* order_dev = nullptr;
+    unsigned long long* cost_dev = nullptr;  // per-tile durations of the launches since the last order
     uint32_t order_stride = 0, order_offset = 0, order_n = 0;
     uint32_t width = 0, height = 0;
     int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
@@ -571,8 +574,13 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     if (const char* t = getenv("PTMI_TAIL_TILES")) s->tail_tiles = (uint32_t)atoi(t);  // testing: small frames with whole tiles
     if (const char* t = getenv("PTMI_TAIL_ITEMS")) s->tail_items = (uint32_t)std::max(1, atoi(t));  // tuning
     if (const char* t = getenv("PTMI_MESH_ITEMS")) s->mesh_items = (uint32_t)std::max(1, atoi(t));  // tuning
+    // Mesh scenes: >= 64 samples per chunk.  It binds only on short sample ranges (a rank's
+    // share): the C4 8-rank shares (256 samples) take 81.3 ms on average with 4 chunks of 64
+    // against 85.4 ms with 7 of 37 (the items' start-up and end-of-item idle lanes), 93.5 ms
+    // with 2 of 128 (a coarser drain); the C5 tile-split shares are flat (profiles/r4/shards).
+    if (hs.flags & 1) s->min_chunk = 64;
     if (const char* t = getenv("PTMI_MIN_CHUNK")) s->min_chunk = (uint32_t)std::max(1, atoi(t));    // tuning
-    if (const char* t = getenv("PTMI_TILE_ORDER")) s->tile_order = atoi(t) != 0;                     // tuning
+    if (const char* t = getenv("PTMI_TILE_ORDER")) s->tile_order = std::max(0, std::min(2, atoi(t)));  // tuning
     if (hs.flags & 1) s->tile_cost = mesh_tile_cost(hs);
     if (const char* t = getenv("PTMI_SPLIT")) s->split = atoi(t) != 0;
     if (const char* t = getenv("PTMI_SPLIT_CHUNK")) s->split_chunk = (uint32_t)std::max(1, atoi(t));
@@ -776,6 +784,7 @@ void ptmi_scene_destroy(ptmi_scene* s) {
     if (s->split_mem) (void)hipFree(s->split_mem);
     if (s->split_host) (void)hipHostFree(s->split_host);
     if (s->order_dev) (void)hipFree(s->order_dev);
+    if (s->cost_dev) (void)hipFree(s->cost_dev);
     for (auto& e : s->events) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
@@ -858,9 +867,16 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     wp.nchunks = chunks;
     wp.chunk_len = chunk_len;
     wp.order = nullptr;
+    wp.cost = nullptr;
     if (!split && s->tile_order && !s->tile_cost.empty() && wp.n_whole == 0 && n_tail > 0) {
-        // Mesh scenes: the chunked tiles' dispatch order, costliest class first (mesh_tile_cost),
-        // raster order within a class; rebuilt when the rank's tile ownership changes.
+        // Mesh scenes: the chunked tiles' dispatch order.  A rank's first launch (or one after
+        // its tile ownership changed) takes the static classes (mesh_tile_cost: costliest
+        // first, raster order within a class); with tile_order 2 every launch also measures
+        // its items and tile_order_kernel writes the next launch's order from those costs.
+        if (s->tile_order == 2 && !s->cost_dev) {
+            HIP_TRY(hipMalloc((void**)&s->cost_dev, (size_t)tiles * sizeof(unsigned long long)));
+            HIP_TRY(hipMemsetAsync(s->cost_dev, 0, (size_t)tiles * sizeof(unsigned long long), st));
+        }
         if (s->order_stride != tile_stride || s->order_offset != tile_offset || s->order_n != n_tail) {
             HIP_TRY(hipStreamSynchronize(st));  // order_host may still feed an earlier copy
             s->order_host.resize(n_tail);
@@ -880,6 +896,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
             s->order_n = n_tail;
         }
         wp.order = s->order_dev;
+        wp.cost = s->tile_order == 2 ? s->cost_dev : nullptr;
     }
     if ((s->flags & 8) && s->dev.cam.aperture != 0 && s->sunf_samples != samples) {  // DoF table for this S
         if (s->sunf) {
@@ -926,6 +943,8 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         HIP_TRY(hipEventRecord(ev1, st));
         s->events.emplace_back(ev0, ev1);
     }
+    // after the timed launch: the next launch's order from this one's item durations
+    if (wp.cost) HIP_TRY(launch_tile_order(wp.cost, wp.n_tail, tile_stride, tile_offset, s->order_dev, st));
     HIP_TRY(launch_reduce(s->partial, sums_dev, wp, (int)W, (int)H, planes, st));
     return PTMI_OK;
 }

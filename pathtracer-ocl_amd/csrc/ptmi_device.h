@@ -236,6 +236,9 @@ struct WorkPlan {
     // round runs chunked tile order[tt] (a permutation of [0, n_tail)); nullptr = identity.
     // The tile keeps its own partial slot, so the sums and their order do not change.
     const uint32_t* order;
+    // Optional per-tile cost accumulator (mesh kernels): each work item adds its duration
+    // (wall-clock ticks) at cost[tile]; tile_order_kernel turns it into the next order.
+    unsigned long long* cost;
 };
 
 }  // namespace ptmi

@@ -2070,7 +2070,16 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
     const unsigned long long tl0 = wall_clock64();
 #endif
     if constexpr ((FL & F_GROUPS) != 0) {
+        const unsigned long long c0 = WP.cost ? wall_clock64() : 0ull;
         trace_groups<FL>(S, samples, WP, seeds, sunf, sums, part);
+        if (WP.cost && threadIdx.x == 0) {  // the item's duration onto its tile (tile_order_kernel)
+            const Item it = work_item(S, WP, blockIdx.x, 0);
+            if (it.ok) {
+                const uint32_t tiles_x = ((uint32_t)S.cam.width + kTile - 1) / kTile;
+                atomicAdd(&WP.cost[(uint32_t)(it.py / kTile) * tiles_x + (uint32_t)(it.px / kTile)],
+                          wall_clock64() - c0);
+            }
+        }
 #if PTMI_TIMELINE
         if (threadIdx.x == 0 && blockIdx.x < ptmi_tl_max) {
             ptmi_tl[2 * blockIdx.x] = tl0;
@@ -2881,6 +2890,44 @@ hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, i
     if (WP.n_tail == 0) return hipSuccess;
     hipLaunchKernelGGL(reduce_chunks_kernel, dim3((WP.n_tail * 64 + 255) / 256), dim3(256), 0, st, part, sums, WP, W,
                        H, planes);
+    return hipGetLastError();
+}
+
+// The next launch's dispatch order of a mesh scene's chunked tiles (WorkPlan::order) from
+// the durations the last launch measured (WorkPlan::cost): costliest first, in 64
+// half-octave classes, any order within a class (the order never changes a result), then
+// the owned tiles' accumulators are cleared.  One workgroup; a few microseconds.
+__global__ __launch_bounds__(1024) void tile_order_kernel(unsigned long long* __restrict__ cost, uint32_t n_tail,
+                                                           uint32_t stride, uint32_t offset, uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[64];
+    const uint32_t t = threadIdx.x;
+    if (t < 64) hist[t] = 0;
+    __syncthreads();
+    auto cls = [&](uint32_t k) {
+        const unsigned long long c = cost[offset + k * stride];
+        const int l2 = 63 - __clzll(c | 1ull);  // floor(log2 c)
+        const int half = (c >> (l2 > 0 ? l2 - 1 : 0)) & 1;  // next bit: half octaves
+        return 63 - min(63, 2 * l2 + half);  // costliest -> class 0
+    };
+    for (uint32_t k = t; k < n_tail; k += blockDim.x) atomicAdd(&hist[cls(k)], 1u);
+    __syncthreads();
+    if (t == 0) {
+        uint32_t run = 0;
+        for (int b = 0; b < 64; b++) {
+            const uint32_t h = hist[b];
+            hist[b] = run;
+            run += h;
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = t; k < n_tail; k += blockDim.x) order[atomicAdd(&hist[cls(k)], 1u)] = k;
+    __syncthreads();
+    for (uint32_t k = t; k < n_tail; k += blockDim.x) cost[offset + k * stride] = 0ull;
+}
+
+hipError_t launch_tile_order(unsigned long long* cost, uint32_t n_tail, uint32_t stride, uint32_t offset,
+                             uint32_t* order, hipStream_t st) {
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, cost, n_tail, stride, offset, order);
     return hipGetLastError();
 }
 
