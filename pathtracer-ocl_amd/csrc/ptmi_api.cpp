@@ -27,8 +27,8 @@ namespace ptmi {
 hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const double* seeds,
                         const double* sunf, double* sums, double* part, hipStream_t st);
 hipError_t launch_sunflower(double* out, uint32_t samples, hipStream_t st);
-hipError_t launch_tile_order(unsigned long long* cost, uint32_t n_tail, uint32_t stride, uint32_t offset,
-                             uint32_t* order, hipStream_t st);
+hipError_t launch_tile_order(unsigned long long* cost, uint32_t n_whole, uint32_t n_tail, uint32_t stride,
+                             uint32_t offset, uint32_t* order, hipStream_t st);
 hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, int W, int H, bool planes,
                          hipStream_t st);
 hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint32_t samples, hipStream_t st);
@@ -70,7 +70,7 @@ struct ptmi_scene {
     std::vector<uint32_t> order_host;
     uint32_t* order_dev = nullptr;
     unsigned long long* cost_dev = nullptr;  // per-tile durations of the launches since the last order
-    uint32_t order_stride = 0, order_offset = 0, order_n = 0;
+    uint32_t order_stride = 0, order_offset = 0, order_n = 0, order_whole = 0, order_cap = 0;
     uint32_t width = 0, height = 0;
     int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
     int hemi_mismatch = 0;  // hemisphere-table records where affine and generic sequences differ (upload_scene)
@@ -868,32 +868,45 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     wp.chunk_len = chunk_len;
     wp.order = nullptr;
     wp.cost = nullptr;
-    if (!split && s->tile_order && !s->tile_cost.empty() && wp.n_whole == 0 && n_tail > 0) {
-        // Mesh scenes: the chunked tiles' dispatch order.  A rank's first launch (or one after
-        // its tile ownership changed) takes the static classes (mesh_tile_cost: costliest
-        // first, raster order within a class); with tile_order 2 every launch also measures
-        // its items and tile_order_kernel writes the next launch's order from those costs.
+    const bool mesh_plan = !s->tile_cost.empty();
+    if (!split && s->tile_order && owned_tiles > 0 && mesh_plan) {
+        // Mesh scenes: the dispatch order of the work items -- whole tiles among themselves,
+        // then each chunk round's tiles among themselves (which tiles are whole and which
+        // chunked stays the raster-defined plan above, so no pixel's sums change).  A rank's
+        // first launch (or one after its tile ownership or plan changed) takes the static
+        // order (mesh_tile_cost's hull-hit classes, costliest first, raster order within a
+        // class); with tile_order 2 every launch also measures its items and
+        // tile_order_kernel writes the next launch's order from those durations.  (The
+        // kernels without meshes do not measure: see item_cost_add.)
         if (s->tile_order == 2 && !s->cost_dev) {
             HIP_TRY(hipMalloc((void**)&s->cost_dev, (size_t)tiles * sizeof(unsigned long long)));
             HIP_TRY(hipMemsetAsync(s->cost_dev, 0, (size_t)tiles * sizeof(unsigned long long), st));
         }
-        if (s->order_stride != tile_stride || s->order_offset != tile_offset || s->order_n != n_tail) {
+        if (s->order_stride != tile_stride || s->order_offset != tile_offset || s->order_n != owned_tiles ||
+            s->order_whole != wp.n_whole) {
             HIP_TRY(hipStreamSynchronize(st));  // order_host may still feed an earlier copy
-            s->order_host.resize(n_tail);
-            for (uint32_t k = 0; k < n_tail; k++) s->order_host[k] = k;
-            std::stable_sort(s->order_host.begin(), s->order_host.end(), [&](uint32_t a, uint32_t b) {
-                return s->tile_cost[tile_offset + a * tile_stride] > s->tile_cost[tile_offset + b * tile_stride];
-            });
-            if (s->order_dev && s->order_n < n_tail) {
+            s->order_host.resize(owned_tiles);
+            for (uint32_t k = 0; k < wp.n_whole; k++) s->order_host[k] = k;
+            for (uint32_t k = 0; k < n_tail; k++) s->order_host[wp.n_whole + k] = k;
+            if (mesh_plan)
+                std::stable_sort(s->order_host.begin() + wp.n_whole, s->order_host.end(), [&](uint32_t a, uint32_t b) {
+                    return s->tile_cost[tile_offset + (wp.n_whole + a) * tile_stride] >
+                           s->tile_cost[tile_offset + (wp.n_whole + b) * tile_stride];
+                });
+            if (s->order_dev && s->order_cap < owned_tiles) {
                 HIP_TRY(hipFree(s->order_dev));
                 s->order_dev = nullptr;
             }
-            if (!s->order_dev) HIP_TRY(hipMalloc((void**)&s->order_dev, (size_t)n_tail * sizeof(uint32_t)));
-            HIP_TRY(hipMemcpyAsync(s->order_dev, s->order_host.data(), (size_t)n_tail * sizeof(uint32_t),
+            if (!s->order_dev) {
+                HIP_TRY(hipMalloc((void**)&s->order_dev, (size_t)owned_tiles * sizeof(uint32_t)));
+                s->order_cap = owned_tiles;
+            }
+            HIP_TRY(hipMemcpyAsync(s->order_dev, s->order_host.data(), (size_t)owned_tiles * sizeof(uint32_t),
                                    hipMemcpyHostToDevice, st));
             s->order_stride = tile_stride;
             s->order_offset = tile_offset;
-            s->order_n = n_tail;
+            s->order_n = owned_tiles;
+            s->order_whole = wp.n_whole;
         }
         wp.order = s->order_dev;
         wp.cost = s->tile_order == 2 ? s->cost_dev : nullptr;
@@ -944,7 +957,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         s->events.emplace_back(ev0, ev1);
     }
     // after the timed launch: the next launch's order from this one's item durations
-    if (wp.cost) HIP_TRY(launch_tile_order(wp.cost, wp.n_tail, tile_stride, tile_offset, s->order_dev, st));
+    if (wp.cost) HIP_TRY(launch_tile_order(wp.cost, wp.n_whole, wp.n_tail, tile_stride, tile_offset, s->order_dev, st));
     HIP_TRY(launch_reduce(s->partial, sums_dev, wp, (int)W, (int)H, planes, st));
     return PTMI_OK;
 }

@@ -232,9 +232,10 @@ struct WorkPlan {
     uint32_t tile_stride, tile_offset;
     uint32_t n_whole, n_tail;
     uint32_t nchunks, chunk_len;
-    // Optional dispatch order of the chunked tiles within each chunk round: item tt of a
-    // round runs chunked tile order[tt] (a permutation of [0, n_tail)); nullptr = identity.
-    // The tile keeps its own partial slot, so the sums and their order do not change.
+    // Optional dispatch order of the chunked tiles within each chunk round: item tq of a
+    // round runs chunked tile order[n_whole + tq] (a permutation of [0, n_tail)); nullptr =
+    // identity.  The tile keeps its own partial slot, so the sums and their order do not
+    // change.  (Entries [0, n_whole) are the identity: whole tiles run in raster order.)
     const uint32_t* order;
     // Optional per-tile cost accumulator (mesh kernels): each work item adds its duration
     // (wall-clock ticks) at cost[tile]; tile_order_kernel turns it into the next order.

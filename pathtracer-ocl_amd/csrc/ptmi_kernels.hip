@@ -1835,7 +1835,7 @@ __device__ __forceinline__ Item work_item(const DevScene& S, const WorkPlan& WP,
         const uint32_t t = item - WP.n_whole;
         const uint32_t c = t / max(WP.n_tail, 1u), tq = t - c * WP.n_tail;
         if (c >= WP.nchunks) return it;
-        const uint32_t tt = WP.order ? WP.order[tq] : tq;  // the round's tq-th tile in dispatch order
+        const uint32_t tt = WP.order ? WP.order[WP.n_whole + tq] : tq;  // the round's tq-th tile in dispatch order
         k = WP.n_whole + tt;
         it.c0 = WP.s_begin + c * WP.chunk_len;
         it.c1 = min(WP.s_end, it.c0 + WP.chunk_len);
@@ -2056,6 +2056,20 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
     store_sums<false>(work_item(S, WP, blockIdx.x, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
 }
 
+// Per-item duration onto its tile's cost accumulator (WorkPlan::cost, tile_order_kernel;
+// mesh kernels only).  The start tick stays in an SGPR pair: kept in LDS it took the mesh
+// kernel past 16 waves per CU (C4 +12.6 %), and any clock read at an item's start cost the
+// C2 kernel 48 B/lane of spill, so the kernels without meshes do not measure.
+__device__ __forceinline__ void item_cost_add(const DevScene& S, const WorkPlan& WP, unsigned long long t0) {
+    if (WP.cost && threadIdx.x == 0) {
+        const Item it = work_item(S, WP, blockIdx.x, 0);
+        if (it.ok) {
+            const uint32_t tiles_x = ((uint32_t)S.cam.width + kTile - 1) / kTile;
+            atomicAdd(&WP.cost[(uint32_t)(it.py / kTile) * tiles_x + (uint32_t)(it.px / kTile)], wall_clock64() - t0);
+        }
+    }
+}
+
 // One wave per workgroup; workgroup b runs work item b of the WorkPlan: an 8x8 tile
 // over the whole sample range (sums -> the frame) or a sample chunk of a tail tile
 // (sums -> its slot of the partial buffer).  A wave that finishes frees its slot (LDS
@@ -2072,14 +2086,7 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
     if constexpr ((FL & F_GROUPS) != 0) {
         const unsigned long long c0 = WP.cost ? wall_clock64() : 0ull;
         trace_groups<FL>(S, samples, WP, seeds, sunf, sums, part);
-        if (WP.cost && threadIdx.x == 0) {  // the item's duration onto its tile (tile_order_kernel)
-            const Item it = work_item(S, WP, blockIdx.x, 0);
-            if (it.ok) {
-                const uint32_t tiles_x = ((uint32_t)S.cam.width + kTile - 1) / kTile;
-                atomicAdd(&WP.cost[(uint32_t)(it.py / kTile) * tiles_x + (uint32_t)(it.px / kTile)],
-                          wall_clock64() - c0);
-            }
-        }
+        item_cost_add(S, WP, c0);
 #if PTMI_TIMELINE
         if (threadIdx.x == 0 && blockIdx.x < ptmi_tl_max) {
             ptmi_tl[2 * blockIdx.x] = tl0;
@@ -2893,41 +2900,46 @@ hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, i
     return hipGetLastError();
 }
 
-// The next launch's dispatch order of a mesh scene's chunked tiles (WorkPlan::order) from
-// the durations the last launch measured (WorkPlan::cost): costliest first, in 64
-// half-octave classes, any order within a class (the order never changes a result), then
-// the owned tiles' accumulators are cleared.  One workgroup; a few microseconds.
-__global__ __launch_bounds__(1024) void tile_order_kernel(unsigned long long* __restrict__ cost, uint32_t n_tail,
-                                                           uint32_t stride, uint32_t offset, uint32_t* __restrict__ order) {
-    __shared__ uint32_t hist[64];
-    const uint32_t t = threadIdx.x;
-    if (t < 64) hist[t] = 0;
+// The next launch's dispatch order (WorkPlan::order) from the durations the last launch
+// measured (WorkPlan::cost): within the whole tiles and within the chunked tiles
+// separately, costliest first in 64 half-octave classes, any order within a class (the
+// order never changes a result); then the owned tiles' accumulators are cleared.  One
+// workgroup; a few microseconds.
+__global__ __launch_bounds__(1024) void tile_order_kernel(unsigned long long* __restrict__ cost, uint32_t n_whole,
+                                                           uint32_t n_tail, uint32_t stride, uint32_t offset,
+                                                           uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[2][64];
+    const uint32_t t = threadIdx.x, n = n_whole + n_tail;
+    if (t < 128) hist[t >> 6][t & 63] = 0;
     __syncthreads();
-    auto cls = [&](uint32_t k) {
-        const unsigned long long c = cost[offset + k * stride];
-        const int l2 = 63 - __clzll(c | 1ull);  // floor(log2 c)
+    auto cls = [&](uint32_t p) {
+        const unsigned long long c = cost[offset + p * stride];
+        const int l2 = 63 - __clzll(c | 1ull);              // floor(log2 c)
         const int half = (c >> (l2 > 0 ? l2 - 1 : 0)) & 1;  // next bit: half octaves
-        return 63 - min(63, 2 * l2 + half);  // costliest -> class 0
+        return 63 - min(63, 2 * l2 + half);                 // costliest -> class 0
     };
-    for (uint32_t k = t; k < n_tail; k += blockDim.x) atomicAdd(&hist[cls(k)], 1u);
+    for (uint32_t p = t; p < n; p += blockDim.x) atomicAdd(&hist[p < n_whole ? 0 : 1][cls(p)], 1u);
     __syncthreads();
-    if (t == 0) {
-        uint32_t run = 0;
+    if (t < 2) {
+        uint32_t run = t == 0 ? 0u : n_whole;
         for (int b = 0; b < 64; b++) {
-            const uint32_t h = hist[b];
-            hist[b] = run;
+            const uint32_t h = hist[t][b];
+            hist[t][b] = run;
             run += h;
         }
     }
     __syncthreads();
-    for (uint32_t k = t; k < n_tail; k += blockDim.x) order[atomicAdd(&hist[cls(k)], 1u)] = k;
+    for (uint32_t p = t; p < n; p += blockDim.x) {
+        const bool w = p < n_whole;
+        order[atomicAdd(&hist[w ? 0 : 1][cls(p)], 1u)] = w ? p : p - n_whole;
+    }
     __syncthreads();
-    for (uint32_t k = t; k < n_tail; k += blockDim.x) cost[offset + k * stride] = 0ull;
+    for (uint32_t p = t; p < n; p += blockDim.x) cost[offset + p * stride] = 0ull;
 }
 
-hipError_t launch_tile_order(unsigned long long* cost, uint32_t n_tail, uint32_t stride, uint32_t offset,
-                             uint32_t* order, hipStream_t st) {
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, cost, n_tail, stride, offset, order);
+hipError_t launch_tile_order(unsigned long long* cost, uint32_t n_whole, uint32_t n_tail, uint32_t stride,
+                             uint32_t offset, uint32_t* order, hipStream_t st) {
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, cost, n_whole, n_tail, stride, offset, order);
     return hipGetLastError();
 }
 

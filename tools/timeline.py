@@ -58,7 +58,8 @@ assert lib.ptmi_diag_timeline_setup(ctypes.c_void_p(buf.data_ptr()), cap, err, l
 render()
 assert lib.ptmi_diag_timeline_setup(None, 0, err, len(err)) == 0, err.value
 t = buf.cpu().numpy().reshape(cap, 2)
-t = t[t[:, 1] > 0].astype(np.float64)
+idx = np.nonzero(t[:, 1] > 0)[0]
+t = t[idx].astype(np.float64)
 n = len(t)
 t0 = t[:, 0].min()
 st, en = (t[:, 0] - t0) * 1e-5, (t[:, 1] - t0) * 1e-5  # ms (100 MHz ticks)
@@ -86,7 +87,16 @@ res = {"config": a.config, "workload": desc, "samples": [s0, s1], "frame_spp": S
        # items in flight at 200 instants, and the start / end of the items by kind (whole
        # tile or chunk: the longest tenth of the items vs the rest)
        "curve": [[round(float(edges[i]), 3), int(act[i])] for i in range(0, 1000, 5)],
+       # the first items in dispatch order (whole tiles in the kernels without meshes)
+       "first_6144_items_ms_p0_p10_p50_p90_p100": [round(float(np.percentile(dur[:6144], q)), 3)
+                                                   for q in (0, 10, 50, 90, 100)],
+       # per XCD, assuming the round-robin placement of workgroups (blockIdx mod 8): the
+       # summed item time and the last end
+       "xcd_busy_over_mean": [round(float(dur[idx % 8 == x].sum() / (dur.sum() / 8)), 4) for x in range(8)],
+       "xcd_last_end_ms": [round(float(en[idx % 8 == x].max()), 3) for x in range(8)],
        "long_items": {"count": int((dur >= np.percentile(dur, 90)).sum()),
+                      "ms_p0_p10_p50_p90_p100": [round(float(np.percentile(dur[dur >= np.percentile(dur, 90)], q)), 3)
+                                                 for q in (0, 10, 50, 90, 100)],
                       "last_end_ms": round(float(en[dur >= np.percentile(dur, 90)].max()), 3),
                       "last_start_ms": round(float(st[dur >= np.percentile(dur, 90)].max()), 3)}}
 print(json.dumps({k: v for k, v in res.items() if k != "curve"}))
