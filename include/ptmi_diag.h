@@ -30,6 +30,14 @@ int ptmi_diag_timeline_setup(void* buf_dev, uint32_t cap, char* err, size_t err_
 int ptmi_diag_walk(ptmi_scene* s, int mode, const void* req_dev, uint32_t n, void* res_dev,
                    uint32_t* counter_dev, void* hip_stream, float* ms, char* err, size_t err_len);
 
+/* Host only (no device call): the static dispatch class of every 8x8 tile of a mesh
+ * scene (ptmi_api.cpp mesh_tile_cost: how many of 9 camera rays through the tile pass a
+ * group object's hull cull, 0..9), raster order, into out[0 .. tiles); all 0 without
+ * meshes.  A rank's first launch dispatches each chunk round's tiles in this order. */
+int ptmi_diag_tile_cost(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
+                        const void* groups, uint32_t n_grp, const void* camera, uint8_t* out, uint32_t n_out,
+                        char* err, size_t err_len);
+
 /* Mesh-scene execution form: enable != 0 renders affine mesh scenes in the split form
  * (trace_split_kernel + walk_split_kernel, pass by pass), 0 (the default) in the
  * one-kernel form (trace_kernel with in-loop walk phases).  Both give the same image

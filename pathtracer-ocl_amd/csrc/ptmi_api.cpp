@@ -1351,6 +1351,30 @@ extern "C" int ptmi_diag_walk(ptmi_scene* s, int mode, const void* req_dev, uint
     return PTMI_OK;
 }
 
+extern "C" int ptmi_diag_tile_cost(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
+                                   const void* groups, uint32_t n_grp, const void* camera, uint8_t* out, uint32_t n_out,
+                                   char* err, size_t err_len) {
+    if (!out) {
+        set_err(err, err_len, "out == NULL");
+        return PTMI_ERR_ARG;
+    }
+    HostScene hs;
+    const int rc = prepare_scene(objects, n_obj, triangles, n_tri, groups, n_grp, camera, nullptr, hs, err, err_len);
+    if (rc) return rc;
+    const uint32_t tiles = (uint32_t)(((hs.cam.width + 7) / 8) * ((hs.cam.height + 7) / 8));
+    if (n_out < tiles) {
+        set_err(err, err_len, "out holds %u tiles, the frame has %u", n_out, tiles);
+        return PTMI_ERR_ARG;
+    }
+    if (hs.flags & 1) {
+        const std::vector<uint8_t> c = mesh_tile_cost(hs);
+        std::memcpy(out, c.data(), tiles);
+    } else {
+        std::memset(out, 0, tiles);
+    }
+    return PTMI_OK;
+}
+
 extern "C" int ptmi_diag_set_split(ptmi_scene* s, int enable) {
     if (!s) return PTMI_ERR_ARG;
     s->split = enable != 0;

@@ -37,6 +37,18 @@ def test_library_exports_every_declared_symbol():
     assert not missing, "not exported with C linkage: %s" % missing
 
 
+def test_library_exports_every_diagnostic_symbol():
+    """include/ptmi_diag.h (diagnostics beside the boundary) is exported too."""
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "ptmi_diag.h")).read(), flags=re.S)
+    declared = sorted(set(re.findall(r"\b(ptmi_diag_[a-z_]+)\s*\(", src)))
+    assert len(declared) >= 7
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib_path()], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    missing = [s for s in declared if s not in exported]
+    assert not missing, "not exported with C linkage: %s" % missing
+
+
 def test_library_loads_and_identifies_gfx950():
     lib = api.load_library()
     for s in _declared():

@@ -65,3 +65,44 @@ def test_node4_chains_fit_the_walk_stack(scene):
         objs, tris, grps, cam = scene_inputs(scene, 64, 48)
     st = _stats(objs, tris, grps, cam)
     assert 1 <= st["depth"] <= 7, st
+
+
+def _tile_cost(objs, tris, grps, cam, w, h):
+    import ctypes
+    import numpy as np
+    from ptmi.api import _ptr, _records, load_library
+    lib = load_library()
+    lib.ptmi_diag_tile_cost.restype = ctypes.c_int
+    lib.ptmi_diag_tile_cost.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                        ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                        ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint32, ctypes.c_char_p,
+                                        ctypes.c_size_t]
+    objs, tris, grps, cam = _records(objs, tris, grps, cam)
+    n = ((w + 7) // 8) * ((h + 7) // 8)
+    out = (ctypes.c_uint8 * n)()
+    err = ctypes.create_string_buffer(512)
+    rc = lib.ptmi_diag_tile_cost(_ptr(objs), len(objs), _ptr(tris), len(tris), _ptr(grps), len(grps), _ptr(cam),
+                                 out, n, err, len(err))
+    assert rc == 0, err.value
+    return np.frombuffer(bytes(out), dtype=np.uint8).reshape((h + 7) // 8, (w + 7) // 8)
+
+
+@pytest.mark.parametrize("scene", ["teapot", "gopher"])
+def test_mesh_tile_classes_mark_the_mesh(scene):
+    """The static dispatch classes of a rank's first launch (ptmi_api.cpp mesh_tile_cost):
+    0..9 camera rays of 9 per tile pass the mesh hulls' cull.  The mesh covers a block of
+    these frames (the teapot's hull 8 %, the gopher's 13 % of the tiles at 320x240), some
+    tiles fully, the frame's corners not at all; the classes only order work items
+    (tests/test_gpu_order.py checks the image)."""
+    w, h = 320, 240
+    objs, tris, grps, cam = scene_inputs(scene, w, h)
+    c = _tile_cost(objs, tris, grps, cam, w, h)
+    assert c.max() == 9 and (c == 9).sum() >= 20, c
+    assert c[0, 0] == 0 and c[-1, -1] == 0 and c[0, -1] == 0
+    assert 0.02 < (c > 0).mean() < 0.9
+
+
+def test_tile_classes_are_zero_without_meshes():
+    w, h = 64, 48
+    objs, tris, grps, cam = scene_inputs("reference", w, h)
+    assert _tile_cost(objs, tris, grps, cam, w, h).max() == 0
