@@ -65,7 +65,10 @@ struct ptmi_scene {
     uint32_t min_chunk = 32;   // fewest samples per chunk item (see render)
     // Mesh scenes: per-tile cost class (mesh_tile_cost) and the dispatch order built from it
     // for the last (tile_stride, tile_offset) rendered (see render).
-    int tile_order = 2;  // 0: raster order, 1: static (hull-hit classes), 2: measured by the last launch
+    // 0: raster order, 1: static (hull-hit classes), 2: measured by the last launch (needs a
+    // build with PTMI_TILE_COST=1 -- see ptmi_kernels.hip item_cost_add; else the order is
+    // arbitrary within the static plan, which never changes a result)
+    int tile_order = 1;
     std::vector<uint8_t> tile_cost;
     std::vector<uint32_t> order_host;
     uint32_t* order_dev = nullptr;

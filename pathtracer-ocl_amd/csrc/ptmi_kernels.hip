@@ -2057,9 +2057,15 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
 }
 
 // Per-item duration onto its tile's cost accumulator (WorkPlan::cost, tile_order_kernel;
-// mesh kernels only).  The start tick stays in an SGPR pair: kept in LDS it took the mesh
-// kernel past 16 waves per CU (C4 +12.6 %), and any clock read at an item's start cost the
-// C2 kernel 48 B/lane of spill, so the kernels without meshes do not measure.
+// mesh kernels only).  Off in the product (PTMI_TILE_COST 0): the clock read at an item's
+// start (s_memrealtime, an intrinsic with side effects) made the uniform-load analysis treat
+// every later global load as clobbered, so the mesh kernel's object and root records went
+// from scalar to vector loads (82 of 108 s_loads; HBM writes 3 -> 57 GB per C4 frame from
+// the extra VGPR pressure and spill).  Kept in LDS the tick cost the mesh kernel its 16th
+// wave per CU; in the kernels without meshes any clock read cost 48 B/lane of spill.
+#ifndef PTMI_TILE_COST
+#define PTMI_TILE_COST 0
+#endif
 __device__ __forceinline__ void item_cost_add(const DevScene& S, const WorkPlan& WP, unsigned long long t0) {
     if (WP.cost && threadIdx.x == 0) {
         const Item it = work_item(S, WP, blockIdx.x, 0);
@@ -2084,9 +2090,13 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
     const unsigned long long tl0 = wall_clock64();
 #endif
     if constexpr ((FL & F_GROUPS) != 0) {
+#if PTMI_TILE_COST
         const unsigned long long c0 = WP.cost ? wall_clock64() : 0ull;
+#endif
         trace_groups<FL>(S, samples, WP, seeds, sunf, sums, part);
+#if PTMI_TILE_COST
         item_cost_add(S, WP, c0);
+#endif
 #if PTMI_TIMELINE
         if (threadIdx.x == 0 && blockIdx.x < ptmi_tl_max) {
             ptmi_tl[2 * blockIdx.x] = tl0;
