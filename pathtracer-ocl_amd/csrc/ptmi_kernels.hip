@@ -634,6 +634,9 @@ __device__ __forceinline__ void tri_uv(const DevTri& T, d4 o, d4 d, double& u, d
 #ifndef PTMI_GROUP_ACM
 #define PTMI_GROUP_ACM 0
 #endif
+#ifndef PTMI_NCUR_LDS
+#define PTMI_NCUR_LDS 1
+#endif
 // Per-lane LDS traversal stack: a Node4 visit pushes <= 3 entries and BVH4 chains are <= 7
 // nodes long (ptmi_bvh.cpp checks it), so a walk holds <= 21 entries.
 static constexpr int kStack = PTMI_STACK;
@@ -1928,7 +1931,15 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
     acc[1 * kBlock] = 0.0;
     acc[2 * kBlock] = 0.0;
     double* acm = kAcm ? acm_lds + tid : nullptr;
-    uint32_t n_gen = it.c0, n_cur = 0;
+    uint32_t n_gen = it.c0;
+#if PTMI_NCUR_LDS
+    // The sample index of the lane's current path waits in LDS (written at path start, read by
+    // the shading's noise draws): in registers the 4-wave budget spilled it, a scratch store at
+    // nearly every loop iteration.
+    __shared__ uint32_t ncur_lds[kBlock];
+#else
+    uint32_t n_cur = 0;
+#endif
     bool buffered = false, active = false, pending = false;
     PathState P;
     PTMI_TSTAMP(t_loop);
@@ -1980,8 +1991,12 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
                 acm[1 * kBlock] = 0.0;
                 acm[2 * kBlock] = 0.0;
             }
+#if PTMI_NCUR_LDS
+            ncur_lds[tid] = n_gen - 1;
+#else
             n_cur = n_gen - 1;
-            if constexpr ((FL & F_XRNG) != 0) P.rng = xseed(seed_bits, n_cur);
+#endif
+            if constexpr ((FL & F_XRNG) != 0) P.rng = xseed(seed_bits, n_gen - 1);
             buffered = false;
             active = true;
         }
@@ -2030,7 +2045,11 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
         }
         PTMI_TADD(14, t_c);
         PTMI_TSTAMP(t_d);
+#if PTMI_NCUR_LDS
+        if (ready && bounce_shade<FL, kAcm>(S, P, h, fgi, ncur_lds[tid], acm)) {
+#else
         if (ready && bounce_shade<FL, kAcm>(S, P, h, fgi, n_cur, acm)) {
+#endif
             if constexpr (kAcm) {
                 acc[0 * kBlock] = acc[0 * kBlock] + acm[0 * kBlock];  // colors += accumColor (tracer.cl:1179)
                 acc[1 * kBlock] = acc[1 * kBlock] + acm[1 * kBlock];
