@@ -73,8 +73,7 @@ struct ptmi_scene {
     std::vector<uint32_t> order_host;
     uint32_t* order_dev = nullptr;
     unsigned long long* cost_dev = nullptr;  // per-tile durations of the launches since the last order
-    uint32_t order_stride = 0, order_offset = 0, order_n = 0, order_whole = 0, order_cap = 0, order_skew = 0;
-    bool tile_skew = true;  // diagonal tile-split ownership where it applies (WorkPlan::skew)
+    uint32_t order_stride = 0, order_offset = 0, order_n = 0, order_whole = 0, order_cap = 0;
     uint32_t width = 0, height = 0;
     int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
     int hemi_mismatch = 0;  // hemisphere-table records where affine and generic sequences differ (upload_scene)
@@ -585,7 +584,6 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     if (hs.flags & 1) s->min_chunk = 64;
     if (const char* t = getenv("PTMI_MIN_CHUNK")) s->min_chunk = (uint32_t)std::max(1, atoi(t));    // tuning
     if (const char* t = getenv("PTMI_TILE_ORDER")) s->tile_order = std::max(0, std::min(2, atoi(t)));  // tuning
-    if (const char* t = getenv("PTMI_TILE_SKEW")) s->tile_skew = atoi(t) != 0;                       // tuning
     if (hs.flags & 1) s->tile_cost = mesh_tile_cost(hs);
     if (const char* t = getenv("PTMI_SPLIT")) s->split = atoi(t) != 0;
     if (const char* t = getenv("PTMI_SPLIT_CHUNK")) s->split_chunk = (uint32_t)std::max(1, atoi(t));
@@ -839,10 +837,6 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     wp.s_end = sample_end;
     wp.tile_stride = tile_stride;
     wp.tile_offset = tile_offset;
-    // Tile split: diagonal ownership when the tile columns divide by the stride (owned_tile);
-    // `t mod N` gave every rank the same columns in every row (C5, 8 ranks: max/mean 1.05).
-    const uint32_t tiles_x = (W + kTile - 1) / kTile;
-    wp.skew = (tile_stride > 1 && s->tile_skew && tiles_x % tile_stride == 0) ? 1u : 0u;
     // Affine mesh scenes in parity mode, when the split form is selected (render_split): pixel-chunks of
     // split_chunk samples (an explicit `chunks` sets the chunk count as for the one-kernel
     // form, so both forms then sum the same chunks in the same order).
@@ -892,15 +886,15 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
             HIP_TRY(hipMemsetAsync(s->cost_dev, 0, (size_t)tiles * sizeof(unsigned long long), st));
         }
         if (s->order_stride != tile_stride || s->order_offset != tile_offset || s->order_n != owned_tiles ||
-            s->order_whole != wp.n_whole || s->order_skew != wp.skew) {
+            s->order_whole != wp.n_whole) {
             HIP_TRY(hipStreamSynchronize(st));  // order_host may still feed an earlier copy
             s->order_host.resize(owned_tiles);
             for (uint32_t k = 0; k < wp.n_whole; k++) s->order_host[k] = k;
             for (uint32_t k = 0; k < n_tail; k++) s->order_host[wp.n_whole + k] = k;
             if (mesh_plan)
                 std::stable_sort(s->order_host.begin() + wp.n_whole, s->order_host.end(), [&](uint32_t a, uint32_t b) {
-                    return s->tile_cost[owned_tile(wp, wp.n_whole + a, tiles_x)] >
-                           s->tile_cost[owned_tile(wp, wp.n_whole + b, tiles_x)];
+                    return s->tile_cost[tile_offset + (wp.n_whole + a) * tile_stride] >
+                           s->tile_cost[tile_offset + (wp.n_whole + b) * tile_stride];
                 });
             if (s->order_dev && s->order_cap < owned_tiles) {
                 HIP_TRY(hipFree(s->order_dev));
@@ -916,7 +910,6 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
             s->order_offset = tile_offset;
             s->order_n = owned_tiles;
             s->order_whole = wp.n_whole;
-            s->order_skew = wp.skew;
         }
         wp.order = s->order_dev;
         wp.cost = s->tile_order == 2 ? s->cost_dev : nullptr;

@@ -240,19 +240,6 @@ struct WorkPlan {
     // Optional per-tile cost accumulator (mesh kernels): each work item adds its duration
     // (wall-clock ticks) at cost[tile]; tile_order_kernel turns it into the next order.
     unsigned long long* cost;
-    // Tile split (tile_stride > 1): 0 = tile t is owned by rank t mod stride; 1 (when the
-    // frame's tile columns divide by the stride) = tile (x, y) by rank (x + y) mod stride, so
-    // a rank's tiles form diagonals instead of the same columns in every row (owned_tile).
-    uint32_t skew;
 };
-
-// The k-th tile a work plan owns (row-major tile index over tiles_x columns).
-__host__ __device__ inline uint32_t owned_tile(const WorkPlan& WP, uint32_t k, uint32_t tiles_x) {
-    if (!WP.skew) return WP.tile_offset + k * WP.tile_stride;
-    const uint32_t m = tiles_x / WP.tile_stride;  // owned tiles per row
-    const uint32_t y = k / m, j = k - y * m;
-    const uint32_t c0 = (WP.tile_offset + WP.tile_stride - y % WP.tile_stride) % WP.tile_stride;
-    return y * tiles_x + c0 + j * WP.tile_stride;
-}
 
 }  // namespace ptmi

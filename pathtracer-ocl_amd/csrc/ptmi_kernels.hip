@@ -1844,7 +1844,7 @@ __device__ __forceinline__ Item work_item(const DevScene& S, const WorkPlan& WP,
         it.c1 = min(WP.s_end, it.c0 + WP.chunk_len);
         it.oslot = ((size_t)c * WP.n_tail + tt) * 64 + lane;
     }
-    const uint32_t tile = owned_tile(WP, k, (uint32_t)tiles_x);
+    const uint32_t tile = WP.tile_offset + k * WP.tile_stride;
     if (tile >= (uint32_t)(tiles_x * tiles_y)) return it;
     it.px = (int)(tile % (uint32_t)tiles_x) * kTile + (lane & 7);
     it.py = (int)(tile / (uint32_t)tiles_x) * kTile + (lane >> 3);
@@ -2458,7 +2458,7 @@ __global__ __launch_bounds__(kBlock, PTMI_WAVES_SPLIT) void trace_split_kernel(D
     // Pixel-chunk q -> pixel and sample range; false for a pixel outside the image.
     auto decode = [&](uint32_t qq, uint32_t& c0) -> bool {
         const uint32_t l = qq & 63u, tc = qq >> 6, c = tc / n_tiles, tk = tc - c * n_tiles;
-        const uint32_t tile = owned_tile(WP, tk, (uint32_t)tiles_x);
+        const uint32_t tile = WP.tile_offset + tk * WP.tile_stride;
         px = (int)(tile % (uint32_t)tiles_x) * kTile + (int)(l & 7u);
         py = (int)(tile / (uint32_t)tiles_x) * kTile + (int)(l >> 3);
         c0 = WP.s_begin + c * WP.chunk_len;
@@ -2801,7 +2801,7 @@ __global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __rest
     if (j >= WP.n_tail * 64) return;
     const uint32_t tt = j >> 6, lane = j & 63;
     const int tiles_x = (W + kTile - 1) / kTile;
-    const uint32_t tile = owned_tile(WP, WP.n_whole + tt, (uint32_t)tiles_x);
+    const uint32_t tile = WP.tile_offset + (WP.n_whole + tt) * WP.tile_stride;
     const int px = (int)(tile % (uint32_t)tiles_x) * kTile + (int)(lane & 7);
     const int py = (int)(tile / (uint32_t)tiles_x) * kTile + (int)(lane >> 3);
     if (px >= W || py >= H) return;

@@ -66,16 +66,12 @@ def shard(rank, world, samples, split):
     raise ValueError("split must be 'sample' or 'tile', got %r" % (split,))
 
 
-def tile_owner_mask(width, height, tile_stride, tile_offset, skew=True):
+def tile_owner_mask(width, height, tile_stride, tile_offset):
     """Boolean (H, W) mask of the pixels a tile-split rank owns: tiles are 8x8,
-    numbered row-major over ceil(W/8) x ceil(H/8) (the kernel's tile index).  When the tile
-    columns divide by the stride, tile (x, y) belongs to rank (x + y) mod stride (diagonals:
-    ptmi_device.h owned_tile, ptmi_api.cpp render), else tile t to rank t mod stride."""
+    numbered row-major over ceil(W/8) x ceil(H/8) (the kernel's tile index)."""
     import numpy as np
     tx = (width + TILE - 1) // TILE
     ys, xs = np.mgrid[0:height, 0:width]
-    if skew and tile_stride > 1 and tx % tile_stride == 0:
-        return ((xs // TILE + ys // TILE) % tile_stride) == tile_offset
     tile = (ys // TILE) * tx + xs // TILE
     return (tile % tile_stride) == tile_offset
 

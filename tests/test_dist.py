@@ -167,19 +167,3 @@ def test_library_and_python_sample_splits_agree(world, samples):
     from ptmi import api
     for g in range(world + 1):
         assert api.sample_split_point(g, world, samples) == pdist.sample_split_point(g, world, samples), (g, world)
-
-
-def test_tile_split_ownership_is_diagonal_where_columns_divide():
-    """Tile split at 8 ranks on the 1280x960 frame (160 tile columns): rank r owns tile
-    (x, y) with (x + y) mod 8 == r -- every rank has 1/8 of every tile column and every
-    tile row, instead of the same 20 columns in every row -- and the ranks partition the
-    frame.  With columns that do not divide by the stride it is t mod stride."""
-    import numpy as np
-    W, H, N = 1280, 960, 8
-    masks = [pdist.tile_owner_mask(W, H, N, r) for r in range(N)]
-    assert np.array_equal(sum(m.astype(int) for m in masks), np.ones((H, W), int))
-    tiles = masks[3][::8, ::8]
-    assert np.all(tiles.sum(axis=0) == tiles.shape[0] // N) and np.all(tiles.sum(axis=1) == tiles.shape[1] // N)
-    odd = pdist.tile_owner_mask(1272, 960, N, 3)[::8, ::8]  # 159 columns: t mod 8
-    t = np.arange(odd.size).reshape(odd.shape)
-    assert np.array_equal(odd, t % N == 3)
