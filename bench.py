@@ -218,7 +218,17 @@ def main():
     ap.add_argument("--extra-steps", type=int, default=2)
     ap.add_argument("--rng", default="noise3d", choices=("noise3d", "xoshiro"),
                     help="xoshiro: the headline config in the opt-in statistical RNG mode (profiling; not `value`)")
+    ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
+                    help="DIAGNOSTIC: a work-plan knob of every scene (ptmi_diag_set_knob; names: tail_tiles, "
+                         "tail_items, mesh_items, min_chunk, tile_order, split_chunk, split_slots, split_sync, "
+                         "split_budget); tuning studies only")
+    ap.add_argument("--split", action="store_true",
+                    help="DIAGNOSTIC: mesh scenes in the split form (needs PTMI_LIB=<the study library>)")
     args = ap.parse_args()
+    knobs = []
+    for kv in args.knob:
+        k, v = kv.split("=", 1)
+        knobs.append((getattr(api, "KNOB_" + k.strip().upper()), int(v)))
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -271,6 +281,11 @@ def main():
             S = samples
         objs, tris, grps, cam = scene_inputs(scene_name, W, H, aper, focal)
         scene = api.Scene(device, objs, tris, grps, cam)
+        for k, v in knobs:  # DIAGNOSTIC tuning (--knob)
+            if scene.set_knob(k, v) != api.PTMI_OK:
+                raise SystemExit("knob %d=%d unsupported by %s" % (k, v, api.LIB_PATH))
+        if args.split and not scene.set_split(True):
+            raise SystemExit("--split needs the study library (PTMI_LIB=pathtracer-ocl_amd/build/libptmi_study.so)")
         if rng:
             scene.set_rng(rng)  # the opt-in statistical mode: never the headline value
         npix = W * H
@@ -405,11 +420,12 @@ def main():
                 l2["measured"] = {"bytes_per_launch": round(mb), "GBs": round(mb / (kms * 1e-3) / 1e9, 1),
                                   "frac": round(mb / (kms * 1e-3) / 1e9 / L2_PEAK_GBS, 4),
                                   "l2_hit_rate": pmc.get("l2_hit_rate"), "source": pmc.get("source")}
-            roof = {"bound": "l2",
-                    "bound_detail": "achieved / peak / frac are the L2 level of the traversal's bytes "
-                                    "(working set L2-resident).  Neither L2 nor HBM binds: the counters show "
-                                    "VALU issue with idle lanes in the BVH walk phases and the latency of "
-                                    "their dependent node loads (roofline.valu, profiles/<round>/SUMMARY.md)",
+            roof = {"bound": "valu_issue_latency",
+                    "bound_detail": "VALU issue with idle lanes in the BVH walk phases and the latency of "
+                                    "their dependent node loads bind (roofline.valu, profiles/<round>/SUMMARY.md); "
+                                    "neither L2 nor HBM does.  achieved / peak / frac are the L2 level of the "
+                                    "traversal's bytes (working set L2-resident), the memory level the "
+                                    "walk's loads are served from; HBM beside it (roofline.hbm)",
                     "achieved": l2["achieved"], "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": l2["frac"],
                     "level": "l2", "l2": l2, "hbm": hbm,
                     "reference_rule": {"bytes_per_sample": round(ac["bytes_per_sample"], 1),

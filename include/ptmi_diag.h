@@ -1,6 +1,8 @@
 /* ptmi_diag.h -- DIAGNOSTIC entry points of libptmi.so (not part of the drop-in
- * boundary, include/ptmi.h): the standalone BVH walk kernels measured against the mesh
- * kernels' in-loop walk phases (tools/walk_bench.py). */
+ * boundary, include/ptmi.h): test hooks, tuning knobs, and the study build's standalone
+ * BVH walk kernels and split execution form (DESIGN.md sections 4-5).  The product
+ * library reads no tuning variable from the environment (PTMI_VERBOSE only); tests and
+ * tuning scripts set the knobs below. */
 #ifndef PTMI_DIAG_H
 #define PTMI_DIAG_H
 #include <stddef.h>
@@ -24,9 +26,11 @@ int ptmi_diag_capture_count(uint32_t* n, char* err, size_t err_len);
  * to buf_dev[2b], buf_dev[2b + 1] for b < cap.  Other builds return PTMI_ERR_UNSUPPORTED. */
 int ptmi_diag_timeline_setup(void* buf_dev, uint32_t cap, char* err, size_t err_len);
 
-/* Walk n requests of scene s with a standalone kernel, results to res_dev; *ms = its
- * time (HIP events on hip_stream).  mode 0: one request per lane (walk_kernel); mode 1:
- * persistent waves with per-lane refill from *counter_dev (walk_pool_kernel). */
+/* Study build only (make -C pathtracer-ocl_amd study -> build/libptmi_study.so; the product
+ * returns PTMI_ERR_UNSUPPORTED): walk n requests of scene s with a standalone kernel,
+ * results to res_dev; *ms = its time (HIP events on hip_stream).  mode 0: one request per
+ * lane (walk_kernel); mode 1: persistent waves with per-lane refill from *counter_dev
+ * (walk_pool_kernel). */
 int ptmi_diag_walk(ptmi_scene* s, int mode, const void* req_dev, uint32_t n, void* res_dev,
                    uint32_t* counter_dev, void* hip_stream, float* ms, char* err, size_t err_len);
 
@@ -38,12 +42,43 @@ int ptmi_diag_tile_cost(const void* objects, uint32_t n_obj, const void* triangl
                         const void* groups, uint32_t n_grp, const void* camera, uint8_t* out, uint32_t n_out,
                         char* err, size_t err_len);
 
-/* Mesh-scene execution form: enable != 0 renders affine mesh scenes in the split form
- * (trace_split_kernel + walk_split_kernel, pass by pass), 0 (the default) in the
- * one-kernel form (trace_kernel with in-loop walk phases).  Both give the same image
- * for the same chunking.  ptmi_diag_split_passes: passes of the last split render. */
+/* Mesh-scene execution form (study build; the product has only the one-kernel form and
+ * returns PTMI_ERR_UNSUPPORTED for enable != 0): enable != 0 renders affine mesh scenes in
+ * the split form (trace_split_kernel + walk_split_kernel, pass by pass), 0 (the default)
+ * in the one-kernel form (trace_kernel with in-loop walk phases).  Both give the same
+ * image for the same chunking.  ptmi_diag_split_passes: passes of the last split render. */
 int ptmi_diag_set_split(ptmi_scene* s, int enable);
 int ptmi_diag_split_passes(const ptmi_scene* s);
+
+/* Work-plan knobs of a resident scene (ptmi_api.cpp ptmi_scene_render); the defaults are
+ * the product's.  TAIL_TILES: chunked tail tiles of an automatic plan in scenes without
+ * meshes (0 = automatic); TAIL_ITEMS / MESH_ITEMS: chunk items per resident wave slot;
+ * MIN_CHUNK: fewest samples per chunk item; TILE_ORDER: dispatch order of a mesh scene's
+ * chunked tiles, 0 raster, 1 costliest static class first (default), 2 from the last
+ * launch's measured item durations (study build only); SPLIT_*: the split form's pool
+ * (study build only).  PTMI_ERR_UNSUPPORTED for a knob or value this build lacks. */
+enum {
+    PTMI_KNOB_TAIL_TILES = 1,
+    PTMI_KNOB_TAIL_ITEMS = 2,
+    PTMI_KNOB_MESH_ITEMS = 3,
+    PTMI_KNOB_MIN_CHUNK = 4,
+    PTMI_KNOB_TILE_ORDER = 5,
+    PTMI_KNOB_SPLIT_CHUNK = 6,
+    PTMI_KNOB_SPLIT_SLOTS = 7,
+    PTMI_KNOB_SPLIT_SYNC = 8,
+    PTMI_KNOB_SPLIT_BUDGET = 9
+};
+int ptmi_diag_set_knob(ptmi_scene* s, int knob, int value);
+
+/* Kernel feature flags (ptmi_kernels.hip F_*) forced onto every scene created after the
+ * call, process-wide; -1 (the default) lets each scene choose.  Test hook: the generic
+ * instantiations must give the specialised ones' images (tests/test_gpu_parity.py). */
+int ptmi_diag_force_flags(int flags);
+
+/* Records of the scene's hemisphere table where the generic (full-operator) sequences
+ * give other bits than the affine ones the table holds (ptmi_kernels.hip
+ * hemi_table_kernel): 0 on a sound toolchain; -1 for a NULL scene. */
+int ptmi_diag_hemi_mismatch(const ptmi_scene* s);
 
 #ifdef __cplusplus
 }

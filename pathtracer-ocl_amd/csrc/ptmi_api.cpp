@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -23,12 +25,16 @@
 #include "ptmi_device.h"
 #include "ptmi_f16.h"
 
+// DIAGNOSTIC study build (make study): the split execution form, the standalone walk
+// kernels and the measured tile order (ptmi_kernels.hip PTMI_STUDY).  The product has 0.
+#ifndef PTMI_STUDY
+#define PTMI_STUDY 0
+#endif
+
 namespace ptmi {
 hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const double* seeds,
                         const double* sunf, double* sums, double* part, hipStream_t st);
 hipError_t launch_sunflower(double* out, uint32_t samples, hipStream_t st);
-hipError_t launch_tile_order(unsigned long long* cost, uint32_t n_whole, uint32_t n_tail, uint32_t stride,
-                             uint32_t offset, uint32_t* order, hipStream_t st);
 hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, int W, int H, bool planes,
                          hipStream_t st);
 hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint32_t samples, hipStream_t st);
@@ -38,17 +44,33 @@ hipError_t launch_hemi_table(double* out, int* mismatch, hipStream_t st);
 hipError_t launch_combine(const double* parts, uint32_t nparts, size_t npix, double* out, uint32_t samples,
                           hipStream_t st);
 const void* trace_kernel_symbol(int flags);
+#if PTMI_STUDY
+hipError_t launch_tile_order(unsigned long long* cost, uint32_t n_whole, uint32_t n_tail, uint32_t stride,
+                             uint32_t offset, uint32_t* order, hipStream_t st);
 bool split_supported(int flags);
 const void* trace_split_symbol(int flags);
 const void* walk_split_symbol();
 hipError_t launch_split_pass(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const SplitBufs& B,
                              const double* seeds, const double* sunf, double* part, uint32_t walk_grid,
                              hipStream_t st);
+#endif
 int trace_block_threads(int flags);
 int trace_tiles_per_block(int flags);
 }  // namespace ptmi
 
 using namespace ptmi;
+
+// What mesh_tile_cost needs of a scene, kept with it so the tile classes are computed on
+// the first render that orders tiles, and only for the tiles that render owns: the camera
+// and, per group object, rows 0-2 of its inverse and its roots' hulls.
+struct TileCostInput {
+    DevCamera cam{};
+    struct Obj {
+        double inv[12];
+        std::vector<std::array<double, 6>> hulls;  // (mn xyz, mx xyz) per root
+    };
+    std::vector<Obj> objs;
+};
 
 struct ptmi_scene {
     int device = 0;
@@ -69,10 +91,11 @@ struct ptmi_scene {
     // build with PTMI_TILE_COST=1 -- see ptmi_kernels.hip item_cost_add; else the order is
     // arbitrary within the static plan, which never changes a result)
     int tile_order = 1;
-    std::vector<uint8_t> tile_cost;
+    TileCostInput tc_in;              // mesh scenes: the inputs of the tile classes
+    std::vector<uint8_t> tile_cost;   // per tile: its class, or kCostUnset until a render needs it
     std::vector<uint32_t> order_host;
     uint32_t* order_dev = nullptr;
-    unsigned long long* cost_dev = nullptr;  // per-tile durations of the launches since the last order
+    unsigned long long* cost_dev = nullptr;  // study build: per-tile durations of the launches since the last order
     uint32_t order_stride = 0, order_offset = 0, order_n = 0, order_whole = 0, order_cap = 0;
     uint32_t width = 0, height = 0;
     int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
@@ -81,20 +104,26 @@ struct ptmi_scene {
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // pending (start, stop) pairs
     std::vector<hipEvent_t> spare;
+#if PTMI_STUDY
     // Split execution of affine mesh scenes (ptmi_kernels.hip trace_split_kernel): a measured
-    // alternative, off by default (3.3x slower than the one-kernel form on C4);
-    // PTMI_SPLIT=1 or ptmi_diag_set_split(s, 1) selects it.
+    // alternative (3.3x slower than the one-kernel form on C4), study build only;
+    // ptmi_diag_set_split(s, 1) selects it, ptmi_diag_set_knob tunes it.
     int split = 0;
-    uint32_t split_chunk = 64;       // samples per pixel-chunk (PTMI_SPLIT_CHUNK)
-    uint32_t split_per_lane = 4;     // slots per tracer lane slot (PTMI_SPLIT_SLOTS)
-    uint32_t split_sync = 8;         // passes between completion checks (PTMI_SPLIT_SYNC)
-    uint32_t split_budget = 4;       // samples a slot starts per pass (PTMI_SPLIT_BUDGET)
+    uint32_t split_chunk = 64;       // samples per pixel-chunk (PTMI_KNOB_SPLIT_CHUNK)
+    uint32_t split_per_lane = 4;     // slots per tracer lane slot (PTMI_KNOB_SPLIT_SLOTS)
+    uint32_t split_sync = 8;         // passes between completion checks (PTMI_KNOB_SPLIT_SYNC)
+    uint32_t split_budget = 4;       // samples a slot starts per pass (PTMI_KNOB_SPLIT_BUDGET)
     SplitBufs sb{};
     void* split_mem = nullptr;
     size_t split_bytes = 0;
     uint32_t* split_host = nullptr;  // pinned: the request count read back at a check
     uint32_t split_passes = 0;       // passes of the last split render (diagnostics)
+#endif
 };
+
+// ptmi_diag_force_flags: kernel flags forced onto every scene created after the call
+// (-1: none).  Test hook for the generic instantiations.
+static std::atomic<int> g_force_flags{-1};
 
 namespace {
 
@@ -366,7 +395,7 @@ int prepare_scene(const void* objects, uint32_t n_obj, const void* triangles, ui
     // instantiation (generic arithmetic + software sampler, tracer.cl:907-914, 1077-1092).
     for (const DevObject& o : hs.objs)
         if ((o.tex && (o.type == 0 || o.type == 1 || o.type == 3)) || (o.tex_nm && o.type == 0)) flags = 63;
-    if (const char* f = getenv("PTMI_FORCE_FLAGS")) flags = atoi(f) & 63;  // testing: force the generic path
+    if (g_force_flags.load() >= 0) flags = g_force_flags.load() & 63;  // ptmi_diag_force_flags (tests)
     if (textures) {
         for (int k = 0; k < 3; k++) {
             const uint64_t texels = (uint64_t)textures->width[k] * textures->height[k] * textures->count[k];
@@ -448,44 +477,76 @@ hipError_t resident_waves(ptmi_scene* s) {
 // Dispatching them first within each chunk round leaves short items for the end.  Only the
 // order of work items changes, never a pixel's sums or their order.  Plain host doubles: a
 // heuristic, not an exactness argument.
-std::vector<uint8_t> mesh_tile_cost(const HostScene& hs) {
-    const DevCamera& c = hs.cam;
-    const int tx = (c.width + 7) / 8, ty = (c.height + 7) / 8;
-    std::vector<uint8_t> cost((size_t)tx * ty, 0);
+constexpr uint8_t kCostUnset = 0xFF;
+
+TileCostInput tile_cost_input(const HostScene& hs) {
+    TileCostInput in;
+    in.cam = hs.cam;
+    for (int j = hs.run_end[3]; j < hs.run_end[4]; j++) {
+        const DevObject& ob = hs.objs[j];
+        TileCostInput::Obj o;
+        std::memcpy(o.inv, ob.inv, sizeof(o.inv));
+        for (int ci = 0; ci < ob.child_count; ci++) {
+            const RootRec& R = hs.root_rec[ob.child_base + ci];
+            o.hulls.push_back({R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1], R.hull_mx[2]});
+        }
+        in.objs.push_back(std::move(o));
+    }
+    return in;
+}
+
+// The class of tile t (raster index).
+uint8_t mesh_tile_class(const TileCostInput& in, const std::vector<std::array<double, 3>>& org, int t) {
+    const DevCamera& c = in.cam;
+    const int tx = (c.width + 7) / 8;
     const double* m = c.inv;
-    for (int t = 0; t < tx * ty; t++) {
-        int hits = 0;
-        for (int q = 0; q < 9; q++) {
-            const double x = (t % tx) * 8 + 1 + 3 * (q % 3) + 0.5, y = (t / tx) * 8 + 1 + 3 * (q / 3) + 0.5;
-            const double a = c.half_width - c.pixel_size * x, b = c.half_height - c.pixel_size * y;
-            double d[3];
-            for (int r = 0; r < 3; r++) d[r] = m[4 * r] * a + m[4 * r + 1] * b - m[4 * r + 2] + m[4 * r + 3] - c.origin[r];
-            bool hit = false;
-            for (int j = hs.run_end[3]; j < hs.run_end[4] && !hit; j++) {
-                const DevObject& ob = hs.objs[j];
-                double o[3], v[3], inv_d[3];
+    int hits = 0;
+    for (int q = 0; q < 9; q++) {
+        const double x = (t % tx) * 8 + 1 + 3 * (q % 3) + 0.5, y = (t / tx) * 8 + 1 + 3 * (q / 3) + 0.5;
+        const double a = c.half_width - c.pixel_size * x, b = c.half_height - c.pixel_size * y;
+        double d[3];
+        for (int r = 0; r < 3; r++) d[r] = m[4 * r] * a + m[4 * r + 1] * b - m[4 * r + 2] + m[4 * r + 3] - c.origin[r];
+        bool hit = false;
+        for (size_t j = 0; j < in.objs.size() && !hit; j++) {
+            const TileCostInput::Obj& ob = in.objs[j];
+            double inv_d[3];
+            for (int r = 0; r < 3; r++) {
+                const double* mi = ob.inv + 4 * r;
+                inv_d[r] = 1.0 / (mi[0] * d[0] + mi[1] * d[1] + mi[2] * d[2]);
+            }
+            for (const auto& H : ob.hulls) {
+                double tn = 0.0, tf = INFINITY;
                 for (int r = 0; r < 3; r++) {
-                    const double* mi = ob.inv + 4 * r;
-                    o[r] = mi[0] * c.origin[0] + mi[1] * c.origin[1] + mi[2] * c.origin[2] + mi[3];
-                    v[r] = mi[0] * d[0] + mi[1] * d[1] + mi[2] * d[2];
-                    inv_d[r] = 1.0 / v[r];
+                    const double t0 = (H[r] - org[j][r]) * inv_d[r], t1 = (H[3 + r] - org[j][r]) * inv_d[r];
+                    tn = std::max(tn, std::min(t0, t1));
+                    tf = std::min(tf, std::max(t0, t1));
                 }
-                for (int ci = 0; ci < ob.child_count && !hit; ci++) {
-                    const RootRec& R = hs.root_rec[ob.child_base + ci];
-                    double tn = 0.0, tf = INFINITY;
-                    for (int r = 0; r < 3; r++) {
-                        const double t0 = (R.hull_mn[r] - o[r]) * inv_d[r], t1 = (R.hull_mx[r] - o[r]) * inv_d[r];
-                        tn = std::max(tn, std::min(t0, t1));
-                        tf = std::min(tf, std::max(t0, t1));
-                    }
-                    hit = tn <= tf;  // NaN slabs (ray in a hull face plane) count as misses: a heuristic
+                if (tn <= tf) {  // NaN slabs (ray in a hull face plane) count as misses: a heuristic
+                    hit = true;
+                    break;
                 }
             }
-            hits += hit ? 1 : 0;
         }
-        cost[t] = (uint8_t)hits;
+        hits += hit ? 1 : 0;
     }
-    return cost;
+    return (uint8_t)hits;
+}
+
+// Classes of the tiles offset, offset + stride, ... not computed yet, into cost (sized to
+// the frame's tiles, kCostUnset where unknown).  The camera origin in each group object's
+// space is computed once per call, not per ray.
+void mesh_tile_cost(const TileCostInput& in, std::vector<uint8_t>& cost, uint32_t stride, uint32_t offset) {
+    const DevCamera& c = in.cam;
+    const size_t tiles = (size_t)((c.width + 7) / 8) * ((c.height + 7) / 8);
+    if (cost.size() != tiles) cost.assign(tiles, kCostUnset);
+    std::vector<std::array<double, 3>> org(in.objs.size());
+    for (size_t j = 0; j < in.objs.size(); j++)
+        for (int r = 0; r < 3; r++) {
+            const double* mi = in.objs[j].inv + 4 * r;
+            org[j][r] = mi[0] * c.origin[0] + mi[1] * c.origin[1] + mi[2] * c.origin[2] + mi[3];
+        }
+    for (size_t t = offset; t < tiles; t += stride)
+        if (cost[t] == kCostUnset) cost[t] = mesh_tile_class(in, org, (int)t);
 }
 
 int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* textures, ptmi_scene** out, char* err,
@@ -558,6 +619,7 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
         // (full-operator) sequences give other bits -- a toolchain or ocml change -- affects
         // no image: it is counted and reported, not a scene failure.
         SCENE_TRY(hipMemcpy(&s->hemi_mismatch, mismatch, sizeof(int), hipMemcpyDeviceToHost));
+        // (ptmi_diag_hemi_mismatch returns the count; tests/test_gpu_rng.py expects 0.)
         if (s->hemi_mismatch && getenv("PTMI_VERBOSE"))
             fprintf(stderr, "ptmi: hemisphere table: %d records where the affine and generic sequences differ "
                             "(generic instantiations compute, they never read the table)\n", s->hemi_mismatch);
@@ -574,22 +636,14 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     s->dev.n_list = hs.n_list;
     s->dev.n_nodes = hs.n_grp;
     s->dev.n_nodes4 = (int32_t)hs.index.nodes.size();
-    if (const char* t = getenv("PTMI_TAIL_TILES")) s->tail_tiles = (uint32_t)atoi(t);  // testing: small frames with whole tiles
-    if (const char* t = getenv("PTMI_TAIL_ITEMS")) s->tail_items = (uint32_t)std::max(1, atoi(t));  // tuning
-    if (const char* t = getenv("PTMI_MESH_ITEMS")) s->mesh_items = (uint32_t)std::max(1, atoi(t));  // tuning
+    // (Tests and tuning studies change the plan through ptmi_diag_set_knob; the library reads
+    // no tuning variable from the environment.)
     // Mesh scenes: >= 64 samples per chunk.  It binds only on short sample ranges (a rank's
     // share): the C4 8-rank shares (256 samples) take 81.3 ms on average with 4 chunks of 64
     // against 85.4 ms with 7 of 37 (the items' start-up and end-of-item idle lanes), 93.5 ms
     // with 2 of 128 (a coarser drain); the C5 tile-split shares are flat (profiles/r4/shards).
     if (hs.flags & 1) s->min_chunk = 64;
-    if (const char* t = getenv("PTMI_MIN_CHUNK")) s->min_chunk = (uint32_t)std::max(1, atoi(t));    // tuning
-    if (const char* t = getenv("PTMI_TILE_ORDER")) s->tile_order = std::max(0, std::min(2, atoi(t)));  // tuning
-    if (hs.flags & 1) s->tile_cost = mesh_tile_cost(hs);
-    if (const char* t = getenv("PTMI_SPLIT")) s->split = atoi(t) != 0;
-    if (const char* t = getenv("PTMI_SPLIT_CHUNK")) s->split_chunk = (uint32_t)std::max(1, atoi(t));
-    if (const char* t = getenv("PTMI_SPLIT_SLOTS")) s->split_per_lane = (uint32_t)std::max(1, atoi(t));
-    if (const char* t = getenv("PTMI_SPLIT_SYNC")) s->split_sync = (uint32_t)std::max(1, atoi(t));
-    if (const char* t = getenv("PTMI_SPLIT_BUDGET")) s->split_budget = (uint32_t)std::max(1, atoi(t));
+    if (hs.flags & 1) s->tc_in = tile_cost_input(hs);  // tile classes: on the first ordered render
     s->dev.n_tri = hs.n_tri;
     s->dev.cam = hs.cam;
     {  // the camera record in device memory (ptmi_kernels.hip camera_ptr)
@@ -604,6 +658,7 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
 }
 
 
+#if PTMI_STUDY
 // Split execution of an affine mesh scene (ptmi_kernels.hip trace_split_kernel): pixel-chunks
 // of chunk_len samples over every owned tile, traced pass by pass by a pool of L path slots
 // (L = the tracer's resident lanes x split_per_lane), each pass followed by the walks it
@@ -681,7 +736,7 @@ int render_split(ptmi_scene* s, uint32_t samples, const WorkPlan& wp, const doub
         }
     }
     s->split_passes = pass;
-    if (getenv("PTMI_SPLIT_DEBUG")) {  // DIAGNOSTIC: slot states after the last pass
+    if (getenv("PTMI_SPLIT_DEBUG")) {  // (study build) slot states after the last pass
         std::vector<uint32_t> it(L);
         HIP_TRY(hipMemcpy2D(it.data(), 4, B.rec + offsetof(SplitRec, u), kSlotBytes, 4, L, hipMemcpyDeviceToHost));
         uint32_t cnt[4];
@@ -694,6 +749,7 @@ int render_split(ptmi_scene* s, uint32_t samples, const WorkPlan& wp, const doub
     (void)sums;
     return PTMI_OK;
 }
+#endif  // PTMI_STUDY
 
 }  // namespace
 
@@ -784,8 +840,10 @@ void ptmi_scene_destroy(ptmi_scene* s) {
         if (b) (void)hipFree(b);
     if (s->partial) (void)hipFree(s->partial);
     if (s->sunf) (void)hipFree(s->sunf);
+#if PTMI_STUDY
     if (s->split_mem) (void)hipFree(s->split_mem);
     if (s->split_host) (void)hipHostFree(s->split_host);
+#endif
     if (s->order_dev) (void)hipFree(s->order_dev);
     if (s->cost_dev) (void)hipFree(s->cost_dev);
     for (auto& e : s->events) {
@@ -841,7 +899,12 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     // split_chunk samples (an explicit `chunks` sets the chunk count as for the one-kernel
     // form, so both forms then sum the same chunks in the same order).
     const int kflags = s->flags | (s->rng == PTMI_RNG_XOSHIRO ? 64 : 0);
+#if PTMI_STUDY
     const bool split = s->split && split_supported(kflags) && range > 0;
+#else
+    constexpr bool split = false;
+#endif
+#if PTMI_STUDY
     if (split) {
         uint32_t nch = chunks ? chunks : (range + s->split_chunk - 1) / s->split_chunk;
         nch = std::max<uint32_t>(1, std::min<uint32_t>(nch, range));
@@ -850,6 +913,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         wp.n_whole = 0;
         wp.n_tail = owned_tiles;
     }
+#endif
     uint32_t n_tail = owned_tiles;
     if (split) {
         chunks = wp.nchunks;
@@ -871,7 +935,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     wp.chunk_len = chunk_len;
     wp.order = nullptr;
     wp.cost = nullptr;
-    const bool mesh_plan = !s->tile_cost.empty();
+    const bool mesh_plan = (s->flags & 1) != 0;  // F_GROUPS
     if (!split && s->tile_order && owned_tiles > 0 && mesh_plan) {
         // Mesh scenes: the dispatch order of the work items -- whole tiles among themselves,
         // then each chunk round's tiles among themselves (which tiles are whole and which
@@ -881,18 +945,20 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         // class); with tile_order 2 every launch also measures its items and
         // tile_order_kernel writes the next launch's order from those durations.  (The
         // kernels without meshes do not measure: see item_cost_add.)
+#if PTMI_STUDY
         if (s->tile_order == 2 && !s->cost_dev) {
             HIP_TRY(hipMalloc((void**)&s->cost_dev, (size_t)tiles * sizeof(unsigned long long)));
             HIP_TRY(hipMemsetAsync(s->cost_dev, 0, (size_t)tiles * sizeof(unsigned long long), st));
         }
+#endif
         if (s->order_stride != tile_stride || s->order_offset != tile_offset || s->order_n != owned_tiles ||
             s->order_whole != wp.n_whole) {
             HIP_TRY(hipStreamSynchronize(st));  // order_host may still feed an earlier copy
+            mesh_tile_cost(s->tc_in, s->tile_cost, tile_stride, tile_offset);  // this render's tiles, once
             s->order_host.resize(owned_tiles);
             for (uint32_t k = 0; k < wp.n_whole; k++) s->order_host[k] = k;
             for (uint32_t k = 0; k < n_tail; k++) s->order_host[wp.n_whole + k] = k;
-            if (mesh_plan)
-                std::stable_sort(s->order_host.begin() + wp.n_whole, s->order_host.end(), [&](uint32_t a, uint32_t b) {
+            std::stable_sort(s->order_host.begin() + wp.n_whole, s->order_host.end(), [&](uint32_t a, uint32_t b) {
                     return s->tile_cost[tile_offset + (wp.n_whole + a) * tile_stride] >
                            s->tile_cost[tile_offset + (wp.n_whole + b) * tile_stride];
                 });
@@ -912,7 +978,9 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
             s->order_whole = wp.n_whole;
         }
         wp.order = s->order_dev;
+#if PTMI_STUDY
         wp.cost = s->tile_order == 2 ? s->cost_dev : nullptr;
+#endif
     }
     if ((s->flags & 8) && s->dev.cam.aperture != 0 && s->sunf_samples != samples) {  // DoF table for this S
         if (s->sunf) {
@@ -949,18 +1017,23 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         s->partial_bytes = need;
     }
     if (ev0) HIP_TRY(hipEventRecord(ev0, st));
+#if PTMI_STUDY
     if (split) {
         const int rc = render_split(s, samples, wp, seeds_dev, sums_dev, st, err, err_len);
         if (rc) return rc;
-    } else {
+    } else
+#endif
+    {
         HIP_TRY(launch_trace(s->dev, kflags, samples, wp, seeds_dev, s->sunf, sums_dev, s->partial, st));
     }
     if (ev1) {
         HIP_TRY(hipEventRecord(ev1, st));
         s->events.emplace_back(ev0, ev1);
     }
+#if PTMI_STUDY
     // after the timed launch: the next launch's order from this one's item durations
     if (wp.cost) HIP_TRY(launch_tile_order(wp.cost, wp.n_whole, wp.n_tail, tile_stride, tile_offset, s->order_dev, st));
+#endif
     HIP_TRY(launch_reduce(s->partial, sums_dev, wp, (int)W, (int)H, planes, st));
     return PTMI_OK;
 }
@@ -1275,11 +1348,13 @@ int stats_read(unsigned long long* out, int reset);
 extern "C" int ptmi_stats_read(unsigned long long* out, int reset) { return ptmi::stats_read(out, reset); }
 #endif
 
-// ---- Diagnostics: standalone BVH walks (include/ptmi_diag.h) -------------------------
+// ---- Diagnostics (include/ptmi_diag.h) -------------------------------------------------
 namespace ptmi {
+#if PTMI_STUDY
 hipError_t launch_walk(const DevScene& S, int flags, int mode, const WalkReq* req, uint32_t n, WalkRes* res,
                        uint32_t* next, uint32_t grid, hipStream_t st);
 const void* walk_kernel_symbol(int mode);
+#endif
 hipError_t capture_setup(WalkReq* req, WalkRes* res, uint32_t cap);
 hipError_t capture_count(uint32_t* n);
 hipError_t timeline_setup(unsigned long long* buf, uint32_t cap);
@@ -1317,6 +1392,11 @@ extern "C" int ptmi_diag_capture_count(uint32_t* n, char* err, size_t err_len) {
 
 extern "C" int ptmi_diag_walk(ptmi_scene* s, int mode, const void* req_dev, uint32_t n, void* res_dev,
                               uint32_t* counter_dev, void* hip_stream, float* ms, char* err, size_t err_len) {
+#if !PTMI_STUDY
+    (void)s, (void)mode, (void)req_dev, (void)n, (void)res_dev, (void)counter_dev, (void)hip_stream, (void)ms;
+    set_err(err, err_len, "the standalone walk kernels are in the study build (make -C pathtracer-ocl_amd study)");
+    return PTMI_ERR_UNSUPPORTED;
+#else
     if (!s || !req_dev || !res_dev || (mode != 0 && mode != 1) || (mode == 1 && !counter_dev)) {
         set_err(err, err_len, "ptmi_diag_walk: bad arguments");
         return PTMI_ERR_ARG;
@@ -1330,7 +1410,6 @@ extern "C" int ptmi_diag_walk(ptmi_scene* s, int mode, const void* req_dev, uint
         int per_cu = 0;
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, walk_kernel_symbol(1), 64, 0));
         grid = (uint32_t)std::max(1, per_cu) * (uint32_t)p.multiProcessorCount;
-        if (const char* g = getenv("PTMI_WALK_GRID_MULT")) grid *= (uint32_t)std::max(1, atoi(g));  // tuning
         HIP_TRY(hipMemsetAsync(counter_dev, 0, sizeof(uint32_t), st));
     }
     hipEvent_t e0, e1;
@@ -1352,6 +1431,7 @@ extern "C" int ptmi_diag_walk(ptmi_scene* s, int mode, const void* req_dev, uint
     HIP_TRY(le);
     if (ms) *ms = t;
     return PTMI_OK;
+#endif
 }
 
 extern "C" int ptmi_diag_tile_cost(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
@@ -1370,7 +1450,8 @@ extern "C" int ptmi_diag_tile_cost(const void* objects, uint32_t n_obj, const vo
         return PTMI_ERR_ARG;
     }
     if (hs.flags & 1) {
-        const std::vector<uint8_t> c = mesh_tile_cost(hs);
+        std::vector<uint8_t> c;
+        mesh_tile_cost(tile_cost_input(hs), c, 1, 0);
         std::memcpy(out, c.data(), tiles);
     } else {
         std::memset(out, 0, tiles);
@@ -1380,8 +1461,51 @@ extern "C" int ptmi_diag_tile_cost(const void* objects, uint32_t n_obj, const vo
 
 extern "C" int ptmi_diag_set_split(ptmi_scene* s, int enable) {
     if (!s) return PTMI_ERR_ARG;
+#if PTMI_STUDY
     s->split = enable != 0;
+    return PTMI_OK;
+#else
+    return enable ? PTMI_ERR_UNSUPPORTED : PTMI_OK;  // the one-kernel form is the only one here
+#endif
+}
+
+extern "C" int ptmi_diag_split_passes(const ptmi_scene* s) {
+#if PTMI_STUDY
+    return s ? (int)s->split_passes : -1;
+#else
+    return s ? 0 : -1;
+#endif
+}
+
+extern "C" int ptmi_diag_set_knob(ptmi_scene* s, int knob, int value) {
+    if (!s) return PTMI_ERR_ARG;
+    const uint32_t pos = (uint32_t)std::max(1, value);
+    switch (knob) {
+    case PTMI_KNOB_TAIL_TILES: s->tail_tiles = (uint32_t)std::max(0, value); return PTMI_OK;
+    case PTMI_KNOB_TAIL_ITEMS: s->tail_items = pos; return PTMI_OK;
+    case PTMI_KNOB_MESH_ITEMS: s->mesh_items = pos; return PTMI_OK;
+    case PTMI_KNOB_MIN_CHUNK: s->min_chunk = pos; return PTMI_OK;
+    case PTMI_KNOB_TILE_ORDER:
+        // 2 (the order measured by the last launch) needs the item timing that only the study
+        // build compiles in (ptmi_kernels.hip PTMI_TILE_COST).
+        if (value < 0 || value > (PTMI_STUDY ? 2 : 1)) return PTMI_ERR_UNSUPPORTED;
+        s->tile_order = value;
+        s->order_n = 0;  // rebuild the order at the next render
+        return PTMI_OK;
+#if PTMI_STUDY
+    case PTMI_KNOB_SPLIT_CHUNK: s->split_chunk = pos; return PTMI_OK;
+    case PTMI_KNOB_SPLIT_SLOTS: s->split_per_lane = pos; return PTMI_OK;
+    case PTMI_KNOB_SPLIT_SYNC: s->split_sync = pos; return PTMI_OK;
+    case PTMI_KNOB_SPLIT_BUDGET: s->split_budget = pos; return PTMI_OK;
+#endif
+    default: return PTMI_ERR_UNSUPPORTED;
+    }
+}
+
+extern "C" int ptmi_diag_force_flags(int flags) {
+    if (flags > 63) return PTMI_ERR_ARG;
+    g_force_flags.store(flags < 0 ? -1 : flags);
     return PTMI_OK;
 }
 
-extern "C" int ptmi_diag_split_passes(const ptmi_scene* s) { return s ? (int)s->split_passes : -1; }
+extern "C" int ptmi_diag_hemi_mismatch(const ptmi_scene* s) { return s ? s->hemi_mismatch : -1; }

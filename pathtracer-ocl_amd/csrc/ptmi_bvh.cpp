@@ -70,8 +70,10 @@ struct Builder {
     double c_tri = 2.0;        // SAH cost of a triangle test relative to a node visit
     int leaf_max = kLeafMax;   // triangles per leaf (<= kLeafMax)
     explicit Builder(std::vector<Prim>& p) : prims(p) {
-        if (const char* e = std::getenv("PTMI_BVH_CTRI")) c_tri = std::atof(e);  // tuning experiments
+#if defined(PTMI_STUDY) && PTMI_STUDY  // study build only: the SAH / leaf-size sweeps (tools/bvh_sweep.sh)
+        if (const char* e = std::getenv("PTMI_BVH_CTRI")) c_tri = std::atof(e);
         if (const char* e = std::getenv("PTMI_BVH_LEAF")) leaf_max = std::max(1, std::min(kLeafMax, std::atoi(e)));
+#endif
     }
 
     int make_leaf(int lo, int hi, const double* mn, const double* mx) {

@@ -82,6 +82,12 @@ __shared__ unsigned long long ptmi_wstat[1][32];
 #ifndef PTMI_TIMELINE
 #define PTMI_TIMELINE 0
 #endif
+// DIAGNOSTIC study build (make study): the standalone walk kernels, the split execution
+// form and the measured tile order -- measured alternatives, compiled
+// out of the product library.
+#ifndef PTMI_STUDY
+#define PTMI_STUDY 0
+#endif
 
 namespace ptmi {
 
@@ -343,24 +349,31 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
     return x;
 }
 #if PTMI_XSEED32
-// The pixel's stream key: its seed's 64 bits folded once per work item (xseed_of), so a
-// path seeds from (key, n) with 32-bit multiplies only: xoshiro128**'s four state words
-// are four independent finalisations of (key, n), eight 32-bit multiplies per path (round
-// 3 took two SplitMix64 draws, four 64-bit multiplies, and a third for the camera).
-typedef uint32_t XSeed;
+// The pixel's stream key: its seed's 64 bits folded once per work item into two 32-bit
+// words (xseed_of), so a path seeds from (key, n) with 32-bit multiplies only.  xoshiro128**'s
+// state words s0 / s1 finalise (key.lo ^ nG) / (key.hi ^ nG), s2 / s3 finalise those mixed
+// with the other key word: eight 32-bit multiplies per path (round 3 took two SplitMix64
+// draws, four 64-bit multiplies, and a third for the camera).  Both key words enter the
+// state (a key of 32 bits alone gave 2^32 streams, so a 1080p x 2048-spp frame,
+// ~4.2e9 paths, reused streams across pixels).
+struct XSeed {
+    uint32_t lo, hi;
+};
 __device__ __forceinline__ XSeed xseed_of(uint64_t seed_bits) {
-    return mix32((uint32_t)seed_bits ^ mix32((uint32_t)(seed_bits >> 32) + 0x9E3779B9u));
+    const uint32_t a = (uint32_t)seed_bits, b = (uint32_t)(seed_bits >> 32);
+    return XSeed{mix32(a ^ mix32(b + 0x9E3779B9u)), mix32(b ^ mix32(a + 0x85EBCA6Bu))};
 }
 __device__ __forceinline__ Xrng xseed(XSeed key, uint32_t n) {
-    const uint32_t x = key ^ (n * 0x9E3779B9u);
-    Xrng r{mix32(x + 0x632BE5ABu), mix32(x + 0x85157AF5u), mix32(x + 0x2545F491u), mix32(x + 0xB5297A4Du)};
+    const uint32_t g = n * 0x9E3779B9u;
+    const uint32_t s0 = mix32((key.lo ^ g) + 0x632BE5ABu), s1 = mix32((key.hi ^ g) + 0x85157AF5u);
+    Xrng r{s0, s1, mix32((s0 ^ key.hi) + 0x2545F491u), mix32((s1 ^ key.lo) + 0xB5297A4Du)};
     if ((r.s0 | r.s1 | r.s2 | r.s3) == 0) r.s0 = 1;  // the all-zero state is the one fixed point
     return r;
 }
 __device__ __forceinline__ void xcamera(XSeed key, uint32_t n, float& rx, float& ry) {
-    const uint32_t x = key ^ (n * 0x9E3779B9u);
-    rx = (float)(mix32(x + 0x68E31DA4u) >> 8) * 0x1p-24f;
-    ry = (float)(mix32(x + 0x1B56C4E9u) >> 8) * 0x1p-24f;
+    const uint32_t g = n * 0x9E3779B9u;
+    rx = (float)(mix32(((key.lo ^ g) + key.hi) ^ 0x68E31DA4u) >> 8) * 0x1p-24f;
+    ry = (float)(mix32(((key.hi ^ g) + key.lo) ^ 0x1B56C4E9u) >> 8) * 0x1p-24f;
 }
 #else
 typedef uint64_t XSeed;
@@ -1328,7 +1341,8 @@ __device__ __forceinline__ void hemi_sqrt(float u2, double& r2s, double& rc) {
 // multiple of ulp(v): of 2^-16 or coarser whenever |v| >= 128, i.e. for all but ~0.2 %
 // of the draws (|sin| < 0.0029).  Record k holds the four values computed by the code
 // above from u = k 2^-16, so a lane reads the bits it would compute (the table kernel
-// checks the affine and generic sequences agree on every record).  Off-grid draws
+// also counts records where the generic sequences differ -- they never read the table --
+// and ptmi_diag_hemi_mismatch reports the count, 0 on this toolchain).  Off-grid draws
 // compute; the statistical mode draws its hemisphere uniforms on the grid (xnext16).
 #ifndef PTMI_HEMI_TAB_GROUPS
 #define PTMI_HEMI_TAB_GROUPS 0  // mesh scenes compute: the 2 MB table competes with the BVH for the 4 MB
@@ -1373,7 +1387,7 @@ __device__ __forceinline__ d4 random_hemisphere(const double* __restrict__ tab, 
 
 // The table: record k = (sin, cos)(2 pi u), sqrt(u), sqrt(1 - u) for u = k 2^-16, from
 // the affine sequences; `mismatch` counts records where the generic (full-operator)
-// sequences give other bits -- the host refuses the scene then (ptmi_api.cpp).
+// sequences give other bits (ptmi_diag_hemi_mismatch; tests/test_gpu_rng.py expects 0).
 __global__ __launch_bounds__(256) void hemi_table_kernel(double* __restrict__ out, int* __restrict__ mismatch) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= kHemiSize) return;
@@ -2083,7 +2097,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
 // the extra VGPR pressure and spill).  Kept in LDS the tick cost the mesh kernel its 16th
 // wave per CU; in the kernels without meshes any clock read cost 48 B/lane of spill.
 #ifndef PTMI_TILE_COST
-#define PTMI_TILE_COST 0
+#define PTMI_TILE_COST PTMI_STUDY  // the study build measures; the product does not
 #endif
 __device__ __forceinline__ void item_cost_add(const DevScene& S, const WorkPlan& WP, unsigned long long t0) {
     if (WP.cost && threadIdx.x == 0) {
@@ -2251,6 +2265,10 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
     }
 }
 
+#if PTMI_STUDY
+// ==== STUDY build only (make study -> build/libptmi_study.so) ==========================
+// The standalone walk kernels and the split execution form of the mesh scenes are the
+// round-4 measurements behind DESIGN.md s5; they are not part of the product library.
 // ---- Standalone BVH walks (round 4) -------------------------------------------------
 // The mesh kernels walk inside their bounce loop, with the whole path state live: 4
 // waves/SIMD, and a walk phase runs ~24 parked lanes of 64 for as long as the longest
@@ -2728,6 +2746,7 @@ const void* walk_kernel_symbol(int mode) {
     return mode == 0 ? reinterpret_cast<const void*>(&walk_kernel<true>)
                      : reinterpret_cast<const void*>(&walk_pool_kernel<true>);
 }
+#endif  // PTMI_STUDY
 
 #if PTMI_CAPTURE
 hipError_t capture_setup(WalkReq* req, WalkRes* res, uint32_t cap) {
@@ -2929,6 +2948,7 @@ hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, i
     return hipGetLastError();
 }
 
+#if PTMI_STUDY  // the measured tile order (needs PTMI_TILE_COST)
 // The next launch's dispatch order (WorkPlan::order) from the durations the last launch
 // measured (WorkPlan::cost): within the whole tiles and within the chunked tiles
 // separately, costliest first in 64 half-octave classes, any order within a class (the
@@ -2971,6 +2991,7 @@ hipError_t launch_tile_order(unsigned long long* cost, uint32_t n_whole, uint32_
     hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, cost, n_whole, n_tail, stride, offset, order);
     return hipGetLastError();
 }
+#endif  // PTMI_STUDY
 
 hipError_t launch_finalize(const double* sums, double* out, uint32_t npix, uint32_t samples, hipStream_t st) {
     hipLaunchKernelGGL(finalize_kernel, dim3((npix + 255) / 256), dim3(256), 0, st, sums, out, npix, samples);

@@ -22,9 +22,15 @@ from .textures import TextureSet
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PTMI_LIB", os.path.join(_HERE, "..", "build", "libptmi.so"))
+# DIAGNOSTIC study library (make -C pathtracer-ocl_amd study): the product plus the split
+# execution form, the standalone walk kernels and the measured tile order.
+STUDY_LIB_PATH = os.path.join(_HERE, "..", "build", "libptmi_study.so")
 
 PTMI_OK, PTMI_ERR_ARG, PTMI_ERR_DEVICE, PTMI_ERR_HIP, PTMI_ERR_UNSUPPORTED, PTMI_ERR_NOMEM = 0, -1, -2, -3, -4, -5
 RNG_NOISE3D, RNG_XOSHIRO = 0, 1  # ptmi_scene_set_rng: parity (default) / opt-in statistical mode
+# ptmi_diag_set_knob (include/ptmi_diag.h): work-plan knobs of a resident scene
+(KNOB_TAIL_TILES, KNOB_TAIL_ITEMS, KNOB_MESH_ITEMS, KNOB_MIN_CHUNK, KNOB_TILE_ORDER, KNOB_SPLIT_CHUNK,
+ KNOB_SPLIT_SLOTS, KNOB_SPLIT_SYNC, KNOB_SPLIT_BUDGET) = range(1, 10)
 
 EXPORTS = ("ptmi_trace", "ptmi_device_count", "ptmi_device_name", "ptmi_scene_create", "ptmi_scene_destroy",
            "ptmi_scene_size", "ptmi_scene_render", "ptmi_finalize", "ptmi_fill_seeds", "ptmi_build_info",
@@ -106,6 +112,12 @@ def load_library(path=None):
     if hasattr(lib, "ptmi_index_stats"):
         lib.ptmi_index_stats.restype = i32
         lib.ptmi_index_stats.argtypes = [vp, u32, vp, u32, vp, u32, vp, ctypes.POINTER(ctypes.c_double), i32, cp, sz]
+    for name, args in (("ptmi_diag_set_knob", [vp, i32, i32]), ("ptmi_diag_force_flags", [i32]),
+                       ("ptmi_diag_hemi_mismatch", [vp]), ("ptmi_diag_set_split", [vp, i32]),
+                       ("ptmi_diag_split_passes", [vp])):
+        if hasattr(lib, name):  # (diagnostic libraries of earlier rounds lack some)
+            getattr(lib, name).restype = i32
+            getattr(lib, name).argtypes = args
     if path is None:
         _lib = lib
     return lib
@@ -217,6 +229,23 @@ def index_stats(objects, triangles, groups, camera):
     return dict(zip(("nodes4", "slots", "box_area", "inf_bounds", "max_scale_exp", "roots", "depth"), list(out)))
 
 
+class force_flags:
+    """Context manager (ptmi_diag_force_flags): scenes created inside it -- by Trace or
+    Scene -- launch the kernel instantiation `flags` instead of their own (test hook for
+    the generic instantiations)."""
+
+    def __init__(self, flags, lib=None):
+        self.flags, self.lib = int(flags), lib or load_library()
+
+    def __enter__(self):
+        _check(self.lib.ptmi_diag_force_flags(self.flags), ctypes.create_string_buffer(b"bad flags"))
+        return self
+
+    def __exit__(self, *exc):
+        self.lib.ptmi_diag_force_flags(-1)
+        return False
+
+
 def sample_split_point(g, n, samples):
     """The library's cost-balanced sample split (ptmi_sample_split_point)."""
     return load_library().ptmi_sample_split_point(int(g), int(n), int(samples))
@@ -226,8 +255,9 @@ class Scene:
     """A scene resident on one device (ptmi_scene_*)."""
 
     def __init__(self, device_index, objects, triangles, groups, camera, textures=None, sphereTextures=None,
-                 cubeTextures=None):
-        self._lib = load_library()
+                 cubeTextures=None, lib=None):
+        # lib: another build of the library (e.g. load_library(STUDY_LIB_PATH)); default the product
+        self._lib = lib or load_library()
         objects, triangles, groups, camera = _records(objects, triangles, groups, camera)
         tex = TextureSet(textures, sphereTextures, cubeTextures)
         handle = ctypes.c_void_p()
@@ -262,17 +292,24 @@ class Scene:
         _check(self._lib.ptmi_scene_set_rng(self._h, int(mode), err, len(err)), err)
 
     def set_split(self, enable=True):
-        """Diagnostics (include/ptmi_diag.h): mesh scenes in the split form or the (default)
-        one-kernel form.  Returns False when the library lacks the switch."""
+        """Diagnostics (include/ptmi_diag.h): mesh scenes in the split form (study library
+        only) or the (default) one-kernel form.  Returns False when the library lacks it."""
         if not hasattr(self._lib, "ptmi_diag_set_split"):
             return False
-        self._lib.ptmi_diag_set_split.argtypes = [ctypes.c_void_p, ctypes.c_int]
         return self._lib.ptmi_diag_set_split(self._h, 1 if enable else 0) == 0
 
     def split_passes(self):
-        self._lib.ptmi_diag_split_passes.restype = ctypes.c_int
-        self._lib.ptmi_diag_split_passes.argtypes = [ctypes.c_void_p]
         return self._lib.ptmi_diag_split_passes(self._h)
+
+    def set_knob(self, knob, value):
+        """ptmi_diag_set_knob: a work-plan knob (KNOB_*); returns the library's status code
+        (PTMI_ERR_UNSUPPORTED for a knob or value this build lacks)."""
+        return self._lib.ptmi_diag_set_knob(self._h, int(knob), int(value))
+
+    def hemi_mismatch(self):
+        """ptmi_diag_hemi_mismatch: hemisphere-table records where the generic operator
+        sequences differ from the affine ones the table holds (0 expected)."""
+        return self._lib.ptmi_diag_hemi_mismatch(self._h)
 
     def set_timing(self, enable=True):
         self._lib.ptmi_scene_set_timing(self._h, 1 if enable else 0)

@@ -49,6 +49,24 @@ def test_library_exports_every_diagnostic_symbol():
     assert not missing, "not exported with C linkage: %s" % missing
 
 
+def test_product_library_holds_only_product_kernels():
+    """The study kernels (standalone walks, the split form, the measured tile order) are in
+    build/libptmi_study.so only: the product's kernels are trace_kernel<FL> and its helpers."""
+    out = subprocess.run(["nm", "-D", "--defined-only", "-C", _lib_path()], capture_output=True, text=True,
+                         check=True).stdout
+    kernels = {k.replace("__device_stub__", "") for k in re.findall(r"ptmi::(\w+_kernel)\b", out)}
+    assert "trace_kernel" in kernels
+    assert kernels <= {"trace_kernel", "reduce_chunks_kernel", "finalize_kernel", "combine_kernel", "seeds_kernel",
+                       "sunflower_kernel", "plane_normals_kernel", "hemi_table_kernel"}, sorted(kernels)
+
+
+def test_product_library_reads_no_tuning_environment():
+    """Plan and kernel choices come from the scene and the diag calls, never the environment:
+    the only PTMI_* variable name in the product library is PTMI_VERBOSE."""
+    names = set(re.findall(rb"PTMI_[A-Z0-9_]+", open(_lib_path(), "rb").read()))
+    assert names <= {b"PTMI_VERBOSE"}, sorted(names)
+
+
 def test_library_loads_and_identifies_gfx950():
     lib = api.load_library()
     for s in _declared():

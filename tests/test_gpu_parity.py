@@ -79,7 +79,7 @@ def test_hip_matches_live_reference(scene, w, h, spp, ap, fl, seed):
 
 @pytest.mark.parametrize("force", ["15", "31"])
 @pytest.mark.parametrize("scene,ap", [("reference", 0.0), ("default", 0.15), ("teapot", 0.0), ("gopher", 0.0)])
-def test_generic_instantiation_matches(monkeypatch, scene, ap, force):
+def test_generic_instantiation_matches(scene, ap, force):
     """The feature-specialised kernel instantiation and the generic ones give
     identical images: 15 = all features compiled in (affine), 31 = all features
     with the literal double4 w-lane arithmetic (the path for non-affine scenes)."""
@@ -87,13 +87,13 @@ def test_generic_instantiation_matches(monkeypatch, scene, ap, force):
     objs, tris, grps, cam = scene_inputs(scene, w, h, ap, 1.6 if ap else 0.0)
     seeds = layout.seeds_go_float64(w * h, 77)
     spec = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
-    monkeypatch.setenv("PTMI_FORCE_FLAGS", force)
-    gen = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    with api.force_flags(int(force)):  # ptmi_diag_force_flags
+        gen = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
     assert np.array_equal(spec, gen)
 
 
 @pytest.mark.parametrize("scene,ap", [("reference", 0.0), ("reference", 0.15), ("teapot", 0.0)])
-def test_affine_cores_match_generic_large(monkeypatch, scene, ap):
+def test_affine_cores_match_generic_large(scene, ap):
     """The affine instantiations' divide / sqrt / rsqrt cores (csrc/ptmi_fp64core.h)
     against the generic instantiation's full compiler expansions over a larger
     frame: 160x120 at 24 spp (~1.8 M paths), images bit-identical."""
@@ -101,8 +101,8 @@ def test_affine_cores_match_generic_large(monkeypatch, scene, ap):
     objs, tris, grps, cam = scene_inputs(scene, w, h, ap, 1.6 if ap else 0.0)
     seeds = layout.seeds_go_float64(w * h, 91)
     spec = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
-    monkeypatch.setenv("PTMI_FORCE_FLAGS", "31")
-    gen = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    with api.force_flags(31):
+        gen = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
     assert np.array_equal(spec, gen)
 
 
@@ -198,13 +198,13 @@ def test_sample_split_and_chunking_invariance():
 
 
 @pytest.mark.parametrize("scene,stride", [("reference", 1), ("reference", 3), ("teapot", 1), ("teapot", 2)])
-def test_whole_tiles_and_chunked_tail(monkeypatch, scene, stride):
+def test_whole_tiles_and_chunked_tail(scene, stride):
     """Automatic work plan (ptmi_device.h WorkPlan): whole-tile items first, the last
-    tiles in sample chunks.  PTMI_TAIL_TILES shrinks the chunked tail so a small frame
+    tiles in sample chunks.  The TAIL_TILES knob shrinks the chunked tail so a small frame
     has both kinds; the frame equals the all-whole render (chunks=1) and each tile-split
     part is zero outside its tiles."""
-    monkeypatch.setenv("PTMI_TAIL_TILES", "5")
     torch, sc = _torch_scene(scene, 72, 40)
+    assert sc.set_knob(api.KNOB_TAIL_TILES, 5) == api.PTMI_OK
     S, n = 70, 72 * 40  # 45 tiles (the last column and row partial)
     seeds = torch.tensor(layout.seeds_go_float64(n, 11), dtype=torch.float64, device="cuda")
     whole = torch.empty(n * 4, dtype=torch.float64, device="cuda")

@@ -80,6 +80,22 @@ def test_sincos_core_bit_identical_every_hemisphere_angle():
     assert m.value == 0, "%d mismatches, first noise bits 0x%08x" % (m.value, f.value)
 
 
+@pytest.mark.parametrize("scene", ["reference", "teapot"])
+def test_hemisphere_table_generic_sequences_agree(scene):
+    """The scene's hemisphere table (ptmi_kernels.hip hemi_table_kernel) holds the affine
+    sequences' (sin, cos)(2 pi u), sqrt(u), sqrt(1 - u); the generic instantiations compute
+    them with the full operators.  Every one of the 2^16 records must agree bit for bit
+    (ptmi_diag_hemi_mismatch): the runtime tripwire for the affine specialisation."""
+    from ptmi import api
+    from tests.scene_inputs import scene_inputs
+    objs, tris, grps, cam = scene_inputs(scene, 32, 24)
+    sc = api.Scene(0, objs, tris, grps, cam)
+    try:
+        assert sc.hemi_mismatch() == 0
+    finally:
+        sc.close()
+
+
 def test_cpu_restatement_replays_gpu_ocml():
     lib = _lib()
     rng = np.random.default_rng(3)

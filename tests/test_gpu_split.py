@@ -3,7 +3,10 @@ DESIGN.md section 5) against the one-kernel form: same chunking -> the same fram
 for bit (every sample of a pixel-chunk runs in order with the same arithmetic; the walks are
 group_walks either way).  The split form is a measured alternative, off by default (DESIGN.md
 section 5); the product's one-kernel form is pinned to the reference by test_gpu_parity.py and
-test_gpu_fullres.py, so equality with it pins the split form too."""
+test_gpu_fullres.py, so equality with it pins the split form too.  The split form lives in
+the study library (make -C pathtracer-ocl_amd study), not in the product."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -12,6 +15,20 @@ from ptmi import api, layout
 from tests.scene_inputs import scene_inputs
 
 pytestmark = pytest.mark.gpu
+
+
+def _study():
+    if not os.path.exists(api.STUDY_LIB_PATH):
+        pytest.fail("libptmi_study.so not built (make -C pathtracer-ocl_amd study)")
+    return api.load_library(api.STUDY_LIB_PATH)
+
+
+def test_product_has_no_split_form():
+    objs, tris, grps, cam = scene_inputs("teapot", 64, 48)
+    scene = api.Scene(0, objs, tris, grps, cam)
+    assert not scene.set_split(True)
+    assert scene.set_split(False)
+    scene.close()
 
 
 def _sums(scene, S, seeds, chunks, split, w, h, s0=0, s1=None, stride=1, off=0):
@@ -31,7 +48,7 @@ def _sums(scene, S, seeds, chunks, split, w, h, s0=0, s1=None, stride=1, off=0):
 ])
 def test_split_equals_one_kernel_form(name, w, h, S, chunks, ap):
     objs, tris, grps, cam = scene_inputs(name, w, h, ap, 1.6 if ap else 0.0)
-    scene = api.Scene(0, objs, tris, grps, cam)
+    scene = api.Scene(0, objs, tris, grps, cam, lib=_study())
     seeds = torch.tensor(layout.seeds_go_float64(w * h, 77), dtype=torch.float64, device="cuda")
     a = _sums(scene, S, seeds, chunks, True, w, h)
     assert scene.split_passes() > 1
@@ -44,7 +61,7 @@ def test_split_sample_range_and_tile_split():
     """Sample sub-ranges and tile ownership (the multi-GPU shards) in the split form."""
     w, h, S = 96, 64, 32
     objs, tris, grps, cam = scene_inputs("teapot", w, h)
-    scene = api.Scene(0, objs, tris, grps, cam)
+    scene = api.Scene(0, objs, tris, grps, cam, lib=_study())
     seeds = torch.tensor(layout.seeds_go_float64(w * h, 78), dtype=torch.float64, device="cuda")
     for kw in ({"s0": 8, "s1": 24}, {"stride": 3, "off": 1}):
         a = _sums(scene, S, seeds, 2, True, w, h, **kw)
@@ -59,7 +76,7 @@ def test_split_pool_smaller_than_the_work():
     pass it was claimed in."""
     w, h, S = 640, 480, 64
     objs, tris, grps, cam = scene_inputs("teapot", w, h)
-    scene = api.Scene(0, objs, tris, grps, cam)
+    scene = api.Scene(0, objs, tris, grps, cam, lib=_study())
     seeds = torch.tensor(layout.seeds_go_float64(w * h, 79), dtype=torch.float64, device="cuda")
     a = _sums(scene, S, seeds, 8, True, w, h)
     b = _sums(scene, S, seeds, 8, False, w, h)
