@@ -2601,7 +2601,7 @@ __global__ __launch_bounds__(kBlock, PTMI_WAVES_SPLIT) void trace_split_kernel(D
                     spent++;
                     const float fgi2 = R().f[1];
                     float rx, ry;
-                    camera_offsets<FL>(fgi, fgi2, 0, n_cur, rx, ry);
+                    camera_offsets<FL>(fgi, fgi2, XSeed{}, n_cur, rx, ry);  // (parity mode only: no key)
                     d4 ro, rd;
                     ray_for_pixel<kDof, A>(camera_ptr(S), sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n_cur, ro, rd);
                     start_path<A, kDof>(P, ro, rd);
