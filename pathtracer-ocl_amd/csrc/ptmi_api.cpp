@@ -44,6 +44,7 @@ hipError_t launch_hemi_table(double* out, int* mismatch, hipStream_t st);
 hipError_t launch_combine(const double* parts, uint32_t nparts, size_t npix, double* out, uint32_t samples,
                           hipStream_t st);
 const void* trace_kernel_symbol(int flags);
+bool tile_list_supported(int flags);
 #if PTMI_STUDY
 hipError_t launch_tile_order(unsigned long long* cost, uint32_t n_whole, uint32_t n_tail, uint32_t stride,
                              uint32_t offset, uint32_t* order, hipStream_t st);
@@ -97,6 +98,12 @@ struct ptmi_scene {
     uint32_t* order_dev = nullptr;
     unsigned long long* cost_dev = nullptr;  // study build: per-tile durations of the launches since the last order
     uint32_t order_stride = 0, order_offset = 0, order_n = 0, order_whole = 0, order_cap = 0;
+    // Tile-split launches of the affine mesh kernels: the owned-tile list (WorkPlan::tiles)
+    // of the last (tile_stride, tile_offset) rendered with one (see owned_tile).
+    std::vector<uint32_t> tlist_host;
+    uint32_t* tlist_dev = nullptr;
+    uint32_t tlist_stride = 0, tlist_offset = 0, tlist_cap = 0;
+    bool order_tlist = false;  // the dispatch order was built for a list launch
     uint32_t width = 0, height = 0;
     int flags = 0;  // scene features -> kernel instantiation (ptmi_kernels.hip F_*)
     int hemi_mismatch = 0;  // hemisphere-table records where affine and generic sequences differ (upload_scene)
@@ -343,6 +350,7 @@ struct HostScene {
     DevCamera cam{};
     int32_t run_end[5] = {};
     int flags = 0;
+    int32_t leaf_bit = kLeafNarrow;  // Node4 child code format (finalize_index_codes)
     uint32_t n_list = 0, n_grp = 0, n_tri = 0;
     int32_t n_planes_y = 0;
 };
@@ -354,6 +362,7 @@ int prepare_scene(const void* objects, uint32_t n_obj, const void* triangles, ui
                            n_grp, (const uint8_t*)camera, hs.objs, hs.roots, hs.nodes, hs.index, hs.root_rec, hs.st,
                            hs.cam, hs.run_end, err, err_len);
     if (rc) return rc;
+    hs.leaf_bit = finalize_index_codes(hs.index, hs.root_rec);
     const DevCamera& cam = hs.cam;
     int flags = 0;
     for (const DevObject& o : hs.objs) {
@@ -391,11 +400,15 @@ int prepare_scene(const void* objects, uint32_t n_obj, const void* triangles, ui
     for (const DevObject& o : hs.objs)
         if (o.type == 1) affine = affine && tame(o.inv);
     if (!affine) flags |= 16;                                           // F_PROJ
+    // Child codes past 16 bits (>= 2^15 Node4s or triangles): the generic instantiations,
+    // whose traversal stack holds 32-bit entries (ptmi_kernels.hip walk_index).
+    if (hs.leaf_bit != kLeafNarrow) flags |= 16;
     // Textured plane/sphere/cube colours or plane normal maps: the one textured
     // instantiation (generic arithmetic + software sampler, tracer.cl:907-914, 1077-1092).
     for (const DevObject& o : hs.objs)
         if ((o.tex && (o.type == 0 || o.type == 1 || o.type == 3)) || (o.tex_nm && o.type == 0)) flags = 63;
     if (g_force_flags.load() >= 0) flags = g_force_flags.load() & 63;  // ptmi_diag_force_flags (tests)
+    if (hs.leaf_bit != kLeafNarrow) flags |= 16;  // (never a 16-bit stack for 31-bit codes)
     if (textures) {
         for (int k = 0; k < 3; k++) {
             const uint64_t texels = (uint64_t)textures->width[k] * textures->height[k] * textures->count[k];
@@ -532,10 +545,11 @@ uint8_t mesh_tile_class(const TileCostInput& in, const std::vector<std::array<do
     return (uint8_t)hits;
 }
 
-// Classes of the tiles offset, offset + stride, ... not computed yet, into cost (sized to
-// the frame's tiles, kCostUnset where unknown).  The camera origin in each group object's
-// space is computed once per call, not per ray.
-void mesh_tile_cost(const TileCostInput& in, std::vector<uint8_t>& cost, uint32_t stride, uint32_t offset) {
+// Classes of the tiles owned(0), owned(1), ... owned(n - 1) not computed yet, into cost
+// (sized to the frame's tiles, kCostUnset where unknown).  The camera origin in each group
+// object's space is computed once per call, not per ray.
+template <typename Owned>
+void mesh_tile_cost(const TileCostInput& in, std::vector<uint8_t>& cost, uint32_t n, Owned owned) {
     const DevCamera& c = in.cam;
     const size_t tiles = (size_t)((c.width + 7) / 8) * ((c.height + 7) / 8);
     if (cost.size() != tiles) cost.assign(tiles, kCostUnset);
@@ -545,8 +559,10 @@ void mesh_tile_cost(const TileCostInput& in, std::vector<uint8_t>& cost, uint32_
             const double* mi = in.objs[j].inv + 4 * r;
             org[j][r] = mi[0] * c.origin[0] + mi[1] * c.origin[1] + mi[2] * c.origin[2] + mi[3];
         }
-    for (size_t t = offset; t < tiles; t += stride)
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t t = owned(k);
         if (cost[t] == kCostUnset) cost[t] = mesh_tile_class(in, org, (int)t);
+    }
 }
 
 int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* textures, ptmi_scene** out, char* err,
@@ -636,6 +652,7 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     s->dev.n_list = hs.n_list;
     s->dev.n_nodes = hs.n_grp;
     s->dev.n_nodes4 = (int32_t)hs.index.nodes.size();
+    s->dev.leaf_bit = hs.leaf_bit;
     // (Tests and tuning studies change the plan through ptmi_diag_set_knob; the library reads
     // no tuning variable from the environment.)
     // Mesh scenes: >= 64 samples per chunk.  It binds only on short sample ranges (a rank's
@@ -785,15 +802,16 @@ int ptmi_index_stats(const void* objects, uint32_t n_obj, const void* triangles,
     for (const RootRec& R : hs.root_rec) {
         st[4] = std::max(st[4], std::log2((double)R.sc));
         std::vector<std::pair<int32_t, int>> todo;  // (Node4, its level)
-        if (R.entry >= 0) todo.push_back({R.entry, 1});
+        const int32_t lb = hs.leaf_bit, empty = lb | ((int32_t)hs.index.tris.size() - 1);  // the sentinel leaf
+        if (R.entry < lb) todo.push_back({R.entry, 1});
         while (!todo.empty()) {  // the root's Node4s (children >= 0 are Node4 indices)
             const auto [ni, lv] = todo.back();
             const Node4& nd = hs.index.nodes[ni];
             todo.pop_back();
             st[6] = std::max(st[6], (double)lv);
             for (int i = 0; i < 4; i++) {
-                if (nd.child[i] == kEmptyChild) continue;
-                if (nd.child[i] >= 0) todo.push_back({nd.child[i], lv + 1});
+                if (nd.child[i] == empty) continue;
+                if (nd.child[i] < lb) todo.push_back({nd.child[i], lv + 1});
                 double e[3];
                 for (int k = 0; k < 3; k++) {
                     const double lo = f16_value(nd.bnd[k][0][i]), hi = f16_value(nd.bnd[k][1][i]);
@@ -845,6 +863,7 @@ void ptmi_scene_destroy(ptmi_scene* s) {
     if (s->split_host) (void)hipHostFree(s->split_host);
 #endif
     if (s->order_dev) (void)hipFree(s->order_dev);
+    if (s->tlist_dev) (void)hipFree(s->tlist_dev);
     if (s->cost_dev) (void)hipFree(s->cost_dev);
     for (auto& e : s->events) {
         (void)hipEventDestroy(e.first);
@@ -874,8 +893,28 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     hipStream_t st = (hipStream_t)hip_stream;
     const uint32_t W = s->width, H = s->height, npix = W * H;
     const uint32_t range = sample_end - sample_begin;
-    const uint32_t tiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-    const uint32_t owned_tiles = (tiles + tile_stride - 1 - tile_offset) / tile_stride;
+    const uint32_t tiles_x = (W + kTile - 1) / kTile, tiles = tiles_x * ((H + kTile - 1) / kTile);
+    const int kflags0 = s->flags | (s->rng == PTMI_RNG_XOSHIRO ? 64 : 0);
+    // Tile ownership of a tile-split launch.  Raster: tiles offset, offset + stride, ...; with
+    // 160 tiles per row (1280 px) and stride 8 that gives every rank the same tile columns in
+    // every row -- vertical stripes, which split a mesh unevenly (C5 8 ranks: max/mean 1.05).
+    // Affine mesh scenes whose tile rows divide by the stride take the diagonal instead --
+    // tile (x, y) belongs to rank (x + y) mod stride, each row holding tiles_x / stride of a
+    // rank's tiles -- through the F_TLIST instantiations (WorkPlan::tiles), so the one-GPU
+    // kernels are untouched (profiles/r5/tile_skew).  Every pixel's sums are the same either way.
+#if PTMI_STUDY
+    const bool study_split = s->split;
+#else
+    constexpr bool study_split = false;
+#endif
+    const bool tlist = tile_stride > 1 && tile_list_supported(kflags0) && tiles_x % tile_stride == 0 && !study_split;
+    const uint32_t per_row = tiles_x / tile_stride;
+    auto owned_tile = [&](uint32_t k) -> uint32_t {
+        if (!tlist) return tile_offset + k * tile_stride;
+        const uint32_t ty = k / per_row, j = k - ty * per_row;
+        return ty * tiles_x + (tile_offset + tile_stride - ty % tile_stride) % tile_stride + j * tile_stride;
+    };
+    const uint32_t owned_tiles = tlist ? tiles / tile_stride : (tiles + tile_stride - 1 - tile_offset) / tile_stride;
     // Work items (WorkPlan, ptmi_device.h).  Automatic (chunks == 0), scenes without
     // meshes: whole tiles first, then the last ~0.5 resident waves' worth of tiles
     // split into sample chunks, so that short items fill the end of the launch (~6 per
@@ -898,7 +937,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     // Affine mesh scenes in parity mode, when the split form is selected (render_split): pixel-chunks of
     // split_chunk samples (an explicit `chunks` sets the chunk count as for the one-kernel
     // form, so both forms then sum the same chunks in the same order).
-    const int kflags = s->flags | (s->rng == PTMI_RNG_XOSHIRO ? 64 : 0);
+    const int kflags = kflags0 | (tlist ? 128 : 0);  // F_TLIST
 #if PTMI_STUDY
     const bool split = s->split && split_supported(kflags) && range > 0;
 #else
@@ -935,6 +974,28 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     wp.chunk_len = chunk_len;
     wp.order = nullptr;
     wp.cost = nullptr;
+    wp.tiles = nullptr;
+    if (tlist) {
+        if (s->tlist_stride != tile_stride || s->tlist_offset != tile_offset || s->tlist_host.size() != owned_tiles) {
+            HIP_TRY(hipStreamSynchronize(st));  // tlist_host may still feed an earlier copy
+            s->tlist_host.resize(owned_tiles);
+            for (uint32_t k = 0; k < owned_tiles; k++) s->tlist_host[k] = owned_tile(k);
+            if (s->tlist_dev && s->tlist_cap < owned_tiles) {
+                HIP_TRY(hipFree(s->tlist_dev));
+                s->tlist_dev = nullptr;
+            }
+            if (!s->tlist_dev) {
+                HIP_TRY(hipMalloc((void**)&s->tlist_dev, (size_t)owned_tiles * sizeof(uint32_t)));
+                s->tlist_cap = owned_tiles;
+            }
+            HIP_TRY(hipMemcpyAsync(s->tlist_dev, s->tlist_host.data(), (size_t)owned_tiles * sizeof(uint32_t),
+                                   hipMemcpyHostToDevice, st));
+            s->tlist_stride = tile_stride;
+            s->tlist_offset = tile_offset;
+            s->order_n = 0;  // the dispatch order indexes owned tiles: rebuild it
+        }
+        wp.tiles = s->tlist_dev;
+    }
     const bool mesh_plan = (s->flags & 1) != 0;  // F_GROUPS
     if (!split && s->tile_order && owned_tiles > 0 && mesh_plan) {
         // Mesh scenes: the dispatch order of the work items -- whole tiles among themselves,
@@ -952,15 +1013,15 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         }
 #endif
         if (s->order_stride != tile_stride || s->order_offset != tile_offset || s->order_n != owned_tiles ||
+            s->order_tlist != tlist ||
             s->order_whole != wp.n_whole) {
             HIP_TRY(hipStreamSynchronize(st));  // order_host may still feed an earlier copy
-            mesh_tile_cost(s->tc_in, s->tile_cost, tile_stride, tile_offset);  // this render's tiles, once
+            mesh_tile_cost(s->tc_in, s->tile_cost, owned_tiles, owned_tile);  // this render's tiles, once
             s->order_host.resize(owned_tiles);
             for (uint32_t k = 0; k < wp.n_whole; k++) s->order_host[k] = k;
             for (uint32_t k = 0; k < n_tail; k++) s->order_host[wp.n_whole + k] = k;
             std::stable_sort(s->order_host.begin() + wp.n_whole, s->order_host.end(), [&](uint32_t a, uint32_t b) {
-                    return s->tile_cost[tile_offset + (wp.n_whole + a) * tile_stride] >
-                           s->tile_cost[tile_offset + (wp.n_whole + b) * tile_stride];
+                    return s->tile_cost[owned_tile(wp.n_whole + a)] > s->tile_cost[owned_tile(wp.n_whole + b)];
                 });
             if (s->order_dev && s->order_cap < owned_tiles) {
                 HIP_TRY(hipFree(s->order_dev));
@@ -975,6 +1036,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
             s->order_stride = tile_stride;
             s->order_offset = tile_offset;
             s->order_n = owned_tiles;
+            s->order_tlist = tlist;
             s->order_whole = wp.n_whole;
         }
         wp.order = s->order_dev;
@@ -1451,7 +1513,7 @@ extern "C" int ptmi_diag_tile_cost(const void* objects, uint32_t n_obj, const vo
     }
     if (hs.flags & 1) {
         std::vector<uint8_t> c;
-        mesh_tile_cost(tile_cost_input(hs), c, 1, 0);
+        mesh_tile_cost(tile_cost_input(hs), c, tiles, [](uint32_t k) { return k; });
         std::memcpy(out, c.data(), tiles);
     } else {
         std::memset(out, 0, tiles);

@@ -185,9 +185,10 @@ struct Builder {
     }
 };
 
-// Leaf entry code shared by Node4::child and the kernel's traversal stack
-// (count 0 never occurs: leaves hold 1..kLeafMax triangles).
-int32_t leaf_code(int32_t first, int32_t count) { return -((first << 3) | count) - 1; }
+// The builder's leaf code (ptmi_device.h Node4): the leaf's first triangle behind the wide
+// leaf bit; its last triangle carries kLastTri.  finalize_index_codes re-codes the whole
+// scene's index once every object is built.
+int32_t leaf_code(int32_t first) { return kLeafWide | first; }
 
 
 }  // namespace
@@ -341,11 +342,12 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
             t.chain = p.chain;
             out.tris.push_back(t);
         }
+        out.tris.back().chain |= kLastTri;  // the leaf ends here (ptmi_kernels.hip leaf_visit)
     }
     (void)tri_base;
     auto code_of = [&](int bi) -> int32_t {
         const BNode& n = B.nodes[bi];
-        return n.left < 0 ? leaf_code(leaf_first[bi], n.count) : -2;  // -2: inner, resolved below
+        return n.left < 0 ? leaf_code(leaf_first[bi]) : -2;  // -2: inner, resolved below
     };
     // Collapse the binary tree to 4-wide nodes (children = grandchildren of
     // inner children), emitted breadth first: the top levels of the first
@@ -402,6 +404,27 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
     }
     rec->bmax = bmax;
     return PTMI_OK;
+}
+
+int32_t finalize_index_codes(RootIndex& idx, std::vector<RootRec>& recs) {
+    // The sentinel: one degenerate triangle (zero edges: |det| = 0 < EPSILON for every finite
+    // ray, and NaN comparisons for a NaN ray), the target of every empty slot.
+    DevTri z{};
+    z.n = 0;
+    z.chain = kLastTri;
+    idx.tris.push_back(z);
+    const int32_t sentinel = (int32_t)idx.tris.size() - 1;
+    const bool narrow = idx.nodes.size() < (size_t)kLeafNarrow && sentinel < kLeafNarrow;
+    const int32_t lb = narrow ? kLeafNarrow : kLeafWide;
+    auto recode = [&](int32_t c) -> int32_t {
+        if (c == kEmptyChild) return lb | sentinel;
+        if (c >= kLeafWide) return lb | (c - kLeafWide);
+        return c;  // a Node4 index
+    };
+    for (Node4& nd : idx.nodes)
+        for (int i = 0; i < 4; i++) nd.child[i] = recode(nd.child[i]);
+    for (RootRec& r : recs) r.entry = recode(r.entry);
+    return lb;
 }
 
 }  // namespace ptmi

@@ -24,4 +24,10 @@ int build_object_index(const uint8_t* tris, const std::vector<DevNode>& nodes, c
                        const std::vector<int32_t>& tri_cnt, const int32_t* roots, int n_roots, const double* gate_mn,
                        const double* gate_mx, RootIndex& out, RootRec* rec, char* err, size_t err_len);
 
+// After every object of a scene is built into `idx` (codes in the builder's wide format):
+// appends the sentinel triangle of the empty slots and re-codes every Node4 child and root
+// entry in the scene's final format (ptmi_device.h Node4).  Returns the leaf bit:
+// kLeafNarrow when every code fits 16 bits, else kLeafWide.
+int32_t finalize_index_codes(RootIndex& idx, std::vector<RootRec>& recs);
+
 }  // namespace ptmi

@@ -61,10 +61,10 @@ struct alignas(16) DevNode {
 static_assert(sizeof(DevNode) == 64, "DevNode must stay 64 B");
 
 // Triangle in traversal-index leaf order; `n` is its index in the reference's
-// triangle list (tie-break order and DevTriShade slot), `chain` locates its gate
-// chain: ChainBox[chain >> 5 .. + (chain & 31)), followed by the chain's core box
-// (the intersection of its boxes) at ChainBox[(chain >> 5) + (chain & 31)]
-// (see ptmi_bvh.cpp and chain_certified).
+// triangle list (tie-break order and DevTriShade slot), `chain` (bit 31 masked off:
+// kLastTri marks a leaf's last triangle) locates its gate chain: ChainBox[chain >> 5 ..
+// + (chain & 31)), followed by the chain's core box (the intersection of its boxes) at
+// ChainBox[(chain >> 5) + (chain & 31)] (see ptmi_bvh.cpp and chain_certified).
 struct alignas(16) DevTri {
     double p1[3];
     double e1[3];
@@ -85,15 +85,24 @@ struct alignas(16) ChainBox {
 // one it ran on float boxes, with the same error bound.  Per axis the four children's
 // minima and maxima share one 16-B row, bnd[axis][0 = min, 1 = max][child], so a lane
 // picks its entry and exit planes by the sign of its ray direction with two selects per
-// 8-B half (node_children).  child[i] is a Node4 index (>= 0), a leaf code
-// -((first << 3) | count) - 1 (triangles [first, first + count) of DevScene::tris),
-// or kEmptyChild.
+// 8-B half (node_children).  child[i] is a child code: a Node4 index (< leaf bit) or
+// leaf bit | first, the leaf's triangles being DevScene::tris[first ..] up to and including
+// the first one whose chain has bit 31 set (kLastTri).  The leaf bit is kLeafNarrow when
+// every code of the scene fits 16 bits (the affine kernels' traversal stack holds 16-bit
+// entries in LDS), else kLeafWide (the generic instantiations, 32-bit entries);
+// DevScene::leaf_bit says which.  An empty slot's code is a leaf of one degenerate
+// triangle (DevScene::tris' last record, kLastTri set): never a candidate, so entering it
+// -- only a NaN ray can -- is harmless, and the walk needs no third case.
 struct alignas(64) Node4 {
     uint16_t bnd[3][2][4];  // [axis][min (rounded toward -inf), max (toward +inf)][child]
     int32_t child[4];
 };
 static_assert(sizeof(Node4) == 64, "Node4 must stay 64 B");
-constexpr int32_t kEmptyChild = INT32_MIN;
+constexpr int32_t kLeafNarrow = 0x8000;      // 16-bit codes: nodes < 2^15, leaves 2^15 | first
+constexpr int32_t kLeafWide = 0x40000000;    // 31-bit codes (and the builder's own format)
+constexpr int32_t kEmptyChild = INT32_MIN;   // the builder's empty slot (ptmi_bvh.cpp), re-coded at upload
+constexpr int32_t kLastTri = INT32_MIN;      // DevTri::chain bit 31: the last triangle of its leaf
+constexpr int32_t kChainMask = 0x7FFFFFFF;
 
 // One BVH root of a group object: the widened hull of all its triangles (the
 // cull test before its walk) and the entry code of its Node4 index.  The Node4
@@ -158,6 +167,7 @@ struct DevScene {
     const ChainBox* chains;
     const DevTri* tris;
     const DevTriShade* tri_shade;
+    int32_t leaf_bit;  // kLeafNarrow or kLeafWide (Node4 child codes)
     uint32_t n_obj;   // intersectable objects in objs[]
     uint32_t n_nodes, n_tri;
     uint32_t n_list;  // numObjects of the reference's list (fgi = seed / numObjects, tracer.cl:840)
@@ -219,7 +229,7 @@ constexpr uint32_t kSlotFree = 0xFFFFFFFFu, kSlotDead = 0xFFFFFFFEu;
 constexpr int kTile = 8;          // a wave64 covers an 8x8 pixel tile
 
 // One launch's work items (trace_kernel, by value).  The owned tiles are
-// tile_offset + k * tile_stride, k = 0, 1, ...  The first n_whole of them are one
+// tile_offset + k * tile_stride, k = 0, 1, ... (or tiles[k], see below)  The first n_whole of them are one
 // item each over the whole sample range [s_begin, s_end), summed straight into the
 // frame; the last n_tail are split into nchunks sample chunks of chunk_len, one
 // item each, whose sums go to a partial buffer (chunk-major: chunk c of tail tile tt,
@@ -240,6 +250,10 @@ struct WorkPlan {
     // Optional per-tile cost accumulator (mesh kernels): each work item adds its duration
     // (wall-clock ticks) at cost[tile]; tile_order_kernel turns it into the next order.
     unsigned long long* cost;
+    // Optional owned-tile list (tile-split launches of the affine mesh kernels, the F_TLIST
+    // instantiations): owned tile k is tiles[k] (raster index) instead of tile_offset +
+    // k * tile_stride.  nullptr in every other launch.
+    const uint32_t* tiles;
 };
 
 }  // namespace ptmi

@@ -467,6 +467,7 @@ enum : int {
     F_ALL = 15,
     F_PROJ = 16,      // not affine (see dotv): the literal double4 arithmetic, generic path only
     F_TEX = 32,       // textured objects: with F_ALL | F_PROJ, the one textured instantiation
+    F_TLIST = 128,    // tile-split launch with an owned-tile list (WorkPlan::tiles): affine mesh kernels only
     F_XRNG = 64       // opt-in statistical mode (ptmi_scene_set_rng): xoshiro128** instead of noise3D,
                       // affine instantiations only; never the parity path
 };
@@ -601,7 +602,7 @@ __device__ __forceinline__ void tri_test(const DevScene& S, const DevTri& T, int
     const double t = f * dt;
     const int n = T.n;
     if (better_tri(h, t, pack_hit(slot, key), n)) {
-        const int c = T.chain;
+        const int c = T.chain & kChainMask;
         // Eager mode admits the hit only if the reference would have tested this
         // triangle: its gate chain (root -> its node) passes the exact line-box
         // tests.  The fast mode takes it tentatively; group_walks verifies the
@@ -645,7 +646,10 @@ __device__ __forceinline__ void tri_uv(const DevTri& T, d4 o, d4 d, double& u, d
 #define PTMI_STACK 24
 #endif
 #ifndef PTMI_GROUP_ACM
-#define PTMI_GROUP_ACM 0
+#define PTMI_GROUP_ACM 1
+#endif
+#ifndef PTMI_GROUP_MASK
+#define PTMI_GROUP_MASK 1
 #endif
 #ifndef PTMI_NCUR_LDS
 #define PTMI_NCUR_LDS 1
@@ -654,16 +658,31 @@ __device__ __forceinline__ void tri_uv(const DevTri& T, d4 o, d4 d, double& u, d
 // nodes long (ptmi_bvh.cpp checks it), so a walk holds <= 21 entries.
 static constexpr int kStack = PTMI_STACK;
 static_assert(kStack >= 21, "the BVH4 depth bound of ptmi_bvh.cpp needs 21 stack entries");
-// The traversal stack's pointer type: LDS (address space 3), so every push and pop is a
+// The traversal stack's pointer types: LDS (address space 3), so every push and pop is a
 // ds_write / ds_read whatever the optimiser makes of the pointer (a loop-carried generic
-// pointer had turned the pop into a flat load).
+// pointer had turned the pop into a flat load).  Entries are child codes (ptmi_device.h
+// Node4): 16 bits in the affine instantiations, whose scenes the host keeps to 16-bit
+// codes (ptmi_bvh.cpp finalize_index_codes; 3 KB of stack per wave instead of 6 KB), 32
+// bits in the generic ones.
 typedef __attribute__((address_space(3))) int LdsInt;
+typedef __attribute__((address_space(3))) uint16_t LdsU16;
 __device__ __forceinline__ LdsInt* lds_ptr(int* p) { return (LdsInt*)p; }
+__device__ __forceinline__ LdsU16* lds_ptr(uint16_t* p) { return (LdsU16*)p; }
+template <bool A>
+using StackEntry = typename std::conditional<A, uint16_t, int>::type;
+// The leaf bit of the codes a stack of entry type E walks: 16-bit entries hold only narrow
+// codes (a literal); 32-bit stacks take the scene's (a scalar).
+template <typename E>
+__device__ __forceinline__ int leaf_bit_of(const DevScene& S) {
+    if constexpr (sizeof(E) == 2) return kLeafNarrow;
+    else return S.leaf_bit;
+}
 
 // The reference's gate for one triangle: every reference node on the path from
 // the walked root to the triangle's node passes intersectRayWithBox
 // (tracer.cl:617-719).  Boxes are contiguous, so their loads are independent.
 __device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o, d4 d) {
+    chain &= kChainMask;  // (bit 31: the leaf's last triangle)
     const d4 r = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z, 0.0);  // recomputed: rare, and keeps r out of the walk
     const ChainBox* B = S.chains + (chain >> 5);
     const int len = chain & 31;
@@ -686,6 +705,7 @@ __device__ __forceinline__ bool verify_chain(const DevScene& S, int chain, d4 o,
 // about 100x the 5 ulps the argument needs (error of o + t*d, plus the division's
 // 2 roundings relative to |mn - o|).  NaN anywhere fails every test: no certificate.
 __device__ __forceinline__ bool chain_certified(const DevScene& S, int chain, d4 o, d4 d, double t) {
+    chain &= kChainMask;
     const ChainBox& C = S.chains[(chain >> 5) + (chain & 31)];
     const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
     bool ok = true;
@@ -816,12 +836,13 @@ __device__ __forceinline__ void node_children(const DevScene& S, int cur, const 
         // missed (tn > tf).  NaN slab values (a NaN ray) drop out of the fmaxf / fminf
         // chains: such a child is entered.  Empty slots hold a point box at +infinity
         // (ptmi_bvh.cpp): both planes +-inf, so tn > tf or tf < 0; entering one would be
-        // harmless (kEmptyChild is neither node nor leaf).
+        // harmless (its code is the sentinel leaf of one degenerate triangle).
         k[i] = child_key(tn > tf ? __builtin_huge_valf() : tn, ch[i]);
     }
 }
 
-__device__ __forceinline__ bool node_visit(const DevScene& S, LdsInt* __restrict__ stk, int cur, int& sp,
+template <typename Stk>
+__device__ __forceinline__ bool node_visit(const DevScene& S, Stk* __restrict__ stk, int cur, int& sp,
                                            const WalkRay& W, float lim, int& next) {
     PTMI_COUNT(1);
     double k[4];
@@ -849,16 +870,17 @@ __device__ __forceinline__ bool node_visit(const DevScene& S, LdsInt* __restrict
     return key_entered(k[0]);
 }
 
-// The triangles of one leaf (code = first << 3 | count).
+// The triangles of one leaf: tris[first ..] through the one marked kLastTri.
 template <bool kVerify>
-__device__ __forceinline__ void leaf_visit(const DevScene& S, int code, int slot, int key, d4 o, d4 d, Hit& h,
+__device__ __forceinline__ void leaf_visit(const DevScene& S, int first, int slot, int key, d4 o, d4 d, Hit& h,
                                            int& vchain) {
     PTMI_WADD(31, 1ull);
-    const int first = code >> 3, end = first + (code & 7);
     PTMI_COUNT(2);
-    for (int i = first; i < end; i++) {
+    for (int i = first;; i++) {
         PTMI_COUNT(3);
-        tri_test<kVerify>(S, S.tris[i], i, o, d, slot, key, h, vchain);
+        const DevTri& T = S.tris[i];
+        tri_test<kVerify>(S, T, i, o, d, slot, key, h, vchain);
+        if (T.chain < 0) break;  // kLastTri
     }
 }
 
@@ -866,9 +888,10 @@ __device__ __forceinline__ void leaf_visit(const DevScene& S, int code, int slot
 // child first, the others pushed far-to-near.  Which triangles are FOUND does
 // not depend on the visiting order or the widened boxes (every triangle that
 // can produce a winning t is reached); ties resolve through better_tri.
-template <bool kVerify>
-__device__ __forceinline__ void walk_index(const DevScene& S, LdsInt* __restrict__ stk, const RootRec& R, int slot,
+template <bool kVerify, typename Stk>
+__device__ __forceinline__ void walk_index(const DevScene& S, Stk* __restrict__ stk, const RootRec& R, int slot,
                                            int key, d4 o, d4 d, d4 rw, Hit& h, int& vchain) {
+    const int lb = leaf_bit_of<Stk>(S);
     const WalkRay W = walk_setup(o, rw, R);  // FP32 slab tests
     float lim = walk_limit(h.t);
     int sp = 0;
@@ -880,11 +903,11 @@ __device__ __forceinline__ void walk_index(const DevScene& S, LdsInt* __restrict
     while (true) {
 #if PTMI_STATS == 1
         n_steps++;
-        n_leaves += (cur < 0 && cur != kEmptyChild) ? 1 : 0;
+        n_leaves += cur >= lb ? 1 : 0;
 #endif
         PTMI_COUNT_ACTIVE(19);  // (stats: wave-level walk loop iterations)
         PTMI_TSTAMP(t_nd);
-        if (cur >= 0) {
+        if (cur < lb) {
             int next;
             const bool down = node_visit(S, stk, cur, sp, W, lim, next);
             PTMI_TADD(29, t_nd);
@@ -892,9 +915,9 @@ __device__ __forceinline__ void walk_index(const DevScene& S, LdsInt* __restrict
                 cur = next;
                 continue;
             }
-        } else if (cur != kEmptyChild) {
+        } else {  // a leaf (an empty slot's sentinel leaf included: only a NaN ray enters one)
             PTMI_TSTAMP(t_lf);
-            leaf_visit<kVerify>(S, -cur - 1, slot, key, o, d, h, vchain);
+            leaf_visit<kVerify>(S, cur - lb, slot, key, o, d, h, vchain);
             lim = walk_limit(h.t);
             PTMI_TADD(30, t_lf);
         }
@@ -1224,8 +1247,8 @@ __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd
 // The walks of every group object for one ray.  kVerify: eager gate checks on
 // each improving candidate (exact by construction, slower: the check runs
 // inside the divergent walk loop).
-template <bool A, bool kVerify>
-__device__ __forceinline__ void group_walks_impl(const DevScene& S, LdsInt* __restrict__ stk, d4 ro, d4 rd, Hit& h,
+template <bool A, bool kVerify, typename Stk>
+__device__ __forceinline__ void group_walks_impl(const DevScene& S, Stk* __restrict__ stk, d4 ro, d4 rd, Hit& h,
                                                  bool& cert) {
     for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
         const DevObject& ob = S.objs[j];
@@ -1260,8 +1283,8 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, LdsInt* __re
 // Only then (a lane whose winner fails -- seen only with degenerate boxes, see
 // tests/adversarial.py) are this ray's walks redone with eager checks.  All
 // lanes verify together after the loop instead of one by one inside it.
-template <bool A>
-__device__ __forceinline__ void group_walks(const DevScene& S, LdsInt* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
+template <bool A, typename Stk>
+__device__ __forceinline__ void group_walks(const DevScene& S, Stk* __restrict__ stk, d4 ro, d4 rd, Hit& h) {
     const Hit h0 = h;
     bool cert = false;
     group_walks_impl<A, false>(S, stk, ro, rd, h, cert);
@@ -1642,9 +1665,12 @@ __device__ __noinline__ d4 plane_normal_map(const DevTexArray T, const DevObject
 // findClosestIntersection).  Returns true when the path has ended.
 // kAccLds: accumColor lives in LDS at acm[0, kBlock, 2 kBlock] instead of P.ar/ag/ab
 // (the kernels without meshes; it changes only on bounces that see emission).
-template <int FL, bool kAccLds = false>
+// kMaskLds: the path's mask (throughput) lives in LDS at msk[0, kBlock, 2 kBlock] instead of
+// P.mr/mg/mb (the mesh kernels, where the 4-wave register budget otherwise spills it with a
+// scratch load and store per bounce).
+template <int FL, bool kAccLds = false, bool kMaskLds = false>
 __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, const Hit& h, float fgi, uint32_t n,
-                                             double* acm = nullptr) {
+                                             double* acm = nullptr, double* msk = nullptr) {
     constexpr bool A = !(FL & F_PROJ);
     constexpr bool kX = (FL & F_XRNG) != 0;
     if (h.pk < 0) return true;  // a miss repeats identically until b == 10 in the reference
@@ -1765,20 +1791,26 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
                 if (ob.tex) textured_color<A>(S.tex[type == 0 ? 0 : type == 1 ? 1 : 2], ob, pos, cr, cg, cb);
             }
         }
+        double mr = P.mr, mg = P.mg, mb = P.mb;
+        if constexpr (kMaskLds) {
+            mr = msk[0 * kBlock];
+            mg = msk[1 * kBlock];
+            mb = msk[2 * kBlock];
+        }
         if constexpr (kAccLds) {
             // accumColor += mask * emission, skipped when every product is +-0: accumColor
             // starts at +0 and is never -0 before its last write (a sum is -0 only if both
             // terms are), so adding +-0 would leave it unchanged.  NaN products are added.
-            const double tr = P.mr * er, tg = P.mg * eg, tb = P.mb * eb;
+            const double tr = mr * er, tg = mg * eg, tb = mb * eb;
             if (!(tr == 0.0 && tg == 0.0 && tb == 0.0)) {
                 acm[0 * kBlock] = acm[0 * kBlock] + tr;
                 acm[1 * kBlock] = acm[1 * kBlock] + tg;
                 acm[2 * kBlock] = acm[2 * kBlock] + tb;
             }
         } else {
-            P.ar = P.ar + P.mr * er;
-            P.ag = P.ag + P.mg * eg;
-            P.ab = P.ab + P.mb * eb;
+            P.ar = P.ar + mr * er;
+            P.ag = P.ag + mg * eg;
+            P.ab = P.ab + mb * eb;
         }
         if (er > 0.0) {
             if (b == 0) {  // the reduction's first record (tracer.cl:1160): records are per bounce, so x == b
@@ -1794,12 +1826,21 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
             }
             P.done = true;
         } else {
-            P.mr = P.mr * cr;
-            P.mg = P.mg * cg;
-            P.mb = P.mb * cb;
-            P.mr = P.mr * cosine;
-            P.mg = P.mg * cosine;
-            P.mb = P.mb * cosine;
+            mr = mr * cr;
+            mg = mg * cg;
+            mb = mb * cb;
+            mr = mr * cosine;
+            mg = mg * cosine;
+            mb = mb * cosine;
+            if constexpr (kMaskLds) {
+                msk[0 * kBlock] = mr;
+                msk[1 * kBlock] = mg;
+                msk[2 * kBlock] = mb;
+            } else {
+                P.mr = mr;
+                P.mg = mg;
+                P.mb = mb;
+            }
         }
     }
     if (!entering && !exiting && !reflecting) P.effective++;
@@ -1836,6 +1877,9 @@ struct Item {
     uint32_t i;    // pixel index (inside only)
     int px, py;
 };
+// kList (F_TLIST instantiations): owned tile k is WP.tiles[k] (a scalar load of a uniform
+// index) instead of tile_offset + k * tile_stride.
+template <bool kList = false>
 __device__ __forceinline__ Item work_item(const DevScene& S, const WorkPlan& WP, uint32_t item, int lane) {
     Item it{};
     const int W = S.cam.width, H = S.cam.height;
@@ -1858,7 +1902,7 @@ __device__ __forceinline__ Item work_item(const DevScene& S, const WorkPlan& WP,
         it.c1 = min(WP.s_end, it.c0 + WP.chunk_len);
         it.oslot = ((size_t)c * WP.n_tail + tt) * 64 + lane;
     }
-    const uint32_t tile = WP.tile_offset + k * WP.tile_stride;
+    const uint32_t tile = kList ? WP.tiles[k] : WP.tile_offset + k * WP.tile_stride;
     if (tile >= (uint32_t)(tiles_x * tiles_y)) return it;
     it.px = (int)(tile % (uint32_t)tiles_x) * kTile + (lane & 7);
     it.py = (int)(tile / (uint32_t)tiles_x) * kTile + (lane >> 3);
@@ -1916,13 +1960,16 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
     // per-pixel colour sums (the same additions in the same order) and a parked lane's
     // primitive best (t, pk), which change once per path or per park, wait in LDS too:
     // registers are what the walk phases need.
-    __shared__ int stk_lds[kStack * kStkStride];
+    __shared__ StackEntry<A> stk_lds[kStack * kStkStride];
     __shared__ double acc_lds[3 * kBlock];
     // accumColor of the lane's current path in LDS (bounce_shade kAccLds), as in the kernels
     // without meshes: it changes only on bounces that see emission, and in registers the
     // 4-wave budget spilled it with a load and a store per bounce.
     constexpr bool kAcm = PTMI_GROUP_ACM != 0;
     __shared__ double acm_lds[kAcm ? 3 * kBlock : 1];
+    // ... and the path's mask (bounce_shade kMaskLds).
+    constexpr bool kMsk = PTMI_GROUP_MASK != 0;
+    __shared__ double msk_lds[kMsk ? 3 * kBlock : 1];
     __shared__ double hp_t_lds[kBlock];
     __shared__ int hp_pk_lds[kBlock];
     __shared__ double cam_lds[kCamComp * kBlock];
@@ -1930,7 +1977,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
 #if PTMI_STATS
     if (lane < 32) ptmi_wstat[0][lane] = 0;
 #endif
-    const Item it = work_item(S, WP, blockIdx.x, lane);
+    const Item it = work_item<(FL & F_TLIST) != 0>(S, WP, blockIdx.x, lane);
     if (!it.ok) return;
     const int px = it.px, py = it.py;
     // fgi / fgi2 (tracer.cl:839-841): double division rounded to float.
@@ -1939,12 +1986,13 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
     const float fgi2 = (float)(seed / (double)samples);
     const XSeed seed_bits = xseed_of((uint64_t)__double_as_longlong(seed));  // statistical mode
     const uint32_t c_end = it.inside ? it.c1 : it.c0;
-    LdsInt* stk = lds_ptr(stk_lds + tid);
+    auto* stk = lds_ptr(stk_lds + tid);
     double* acc = acc_lds + tid;
     acc[0 * kBlock] = 0.0;
     acc[1 * kBlock] = 0.0;
     acc[2 * kBlock] = 0.0;
     double* acm = kAcm ? acm_lds + tid : nullptr;
+    double* msk = kMsk ? msk_lds + tid : nullptr;
     uint32_t n_gen = it.c0;
 #if PTMI_NCUR_LDS
     // The sample index of the lane's current path waits in LDS (written at path start, read by
@@ -2005,6 +2053,11 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
                 acm[1 * kBlock] = 0.0;
                 acm[2 * kBlock] = 0.0;
             }
+            if constexpr (kMsk) {
+                msk[0 * kBlock] = 1.0;
+                msk[1 * kBlock] = 1.0;
+                msk[2 * kBlock] = 1.0;
+            }
 #if PTMI_NCUR_LDS
             ncur_lds[tid] = n_gen - 1;
 #else
@@ -2060,9 +2113,9 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
         PTMI_TADD(14, t_c);
         PTMI_TSTAMP(t_d);
 #if PTMI_NCUR_LDS
-        if (ready && bounce_shade<FL, kAcm>(S, P, h, fgi, ncur_lds[tid], acm)) {
+        if (ready && bounce_shade<FL, kAcm, kMsk>(S, P, h, fgi, ncur_lds[tid], acm, msk)) {
 #else
-        if (ready && bounce_shade<FL, kAcm>(S, P, h, fgi, n_cur, acm)) {
+        if (ready && bounce_shade<FL, kAcm, kMsk>(S, P, h, fgi, n_cur, acm, msk)) {
 #endif
             if constexpr (kAcm) {
                 acc[0 * kBlock] = acc[0 * kBlock] + acm[0 * kBlock];  // colors += accumColor (tracer.cl:1179)
@@ -2086,7 +2139,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
 #endif
     // The work item is re-derived (a few integer operations) rather than kept live across
     // the loop: its fields would hold ~5 VGPRs through every walk phase.
-    store_sums<false>(work_item(S, WP, blockIdx.x, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
+    store_sums<false>(work_item<(FL & F_TLIST) != 0>(S, WP, blockIdx.x, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
 }
 
 // Per-item duration onto its tile's cost accumulator (WorkPlan::cost, tile_order_kernel;
@@ -2313,7 +2366,8 @@ __global__ __launch_bounds__(kBlock, PTMI_WALK_WAVES) void walk_pool_kernel(DevS
     enum : int { kIdle = 0, kWalk = 1, kDone = 2, kDrained = 3 };
     int phase = kIdle;
     uint32_t ri = 0;
-    int j = 0, cur = kEmptyChild, sp = 0, vchain = -1;
+    const int lb = S.leaf_bit;
+    int j = 0, cur = lb, sp = 0, vchain = -1;
     bool cert = false;
     d4 o = mk(0.0, 0.0, 0.0, 1.0), d = mk(0.0, 0.0, 0.0, 0.0);
     WalkRay W{};
@@ -2386,12 +2440,12 @@ __global__ __launch_bounds__(kBlock, PTMI_WALK_WAVES) void walk_pool_kernel(DevS
         if (!__any(phase == kWalk || phase == kDone)) break;
         if (phase == kWalk) {  // one walk step of object j (walk_index's loop body)
             bool down = false;
-            if (cur >= 0) {
+            if (cur < lb) {
                 int nxt;
                 down = node_visit(S, stk, cur, sp, W, lim, nxt);
                 if (down) cur = nxt;
-            } else if (cur != kEmptyChild) {
-                leaf_visit<false>(S, -cur - 1, j, S.objs[j].key, o, d, h, vchain);
+            } else {
+                leaf_visit<false>(S, cur - lb, j, S.objs[j].key, o, d, h, vchain);
                 lim = walk_limit(h.t);
             }
             if (!down) {
@@ -2820,7 +2874,8 @@ __global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __rest
     if (j >= WP.n_tail * 64) return;
     const uint32_t tt = j >> 6, lane = j & 63;
     const int tiles_x = (W + kTile - 1) / kTile;
-    const uint32_t tile = WP.tile_offset + (WP.n_whole + tt) * WP.tile_stride;
+    const uint32_t k = WP.n_whole + tt;
+    const uint32_t tile = WP.tiles ? WP.tiles[k] : WP.tile_offset + k * WP.tile_stride;
     const int px = (int)(tile % (uint32_t)tiles_x) * kTile + (int)(lane & 7);
     const int py = (int)(tile / (uint32_t)tiles_x) * kTile + (int)(lane >> 3);
     if (px >= W || py >= H) return;
@@ -2903,7 +2958,13 @@ int trace_tiles_per_block(int flags) { return 1; }
 static int kernel_flags(int flags) {
     if (flags & F_TEX) return F_ALL | F_PROJ | F_TEX;
     if (flags & F_PROJ) return F_ALL | F_PROJ;
+    if ((flags & F_TLIST) && (flags & F_GROUPS) && !(flags & F_XRNG)) return flags & (F_ALL | F_TLIST);
     return flags & (F_ALL | F_XRNG);
+}
+
+// Whether a launch with these scene flags can take an owned-tile list (ptmi_api.cpp render).
+bool tile_list_supported(int flags) {
+    return (flags & F_GROUPS) && !(flags & (F_PROJ | F_TEX | F_XRNG));
 }
 
 const void* trace_kernel_symbol(int flags) {
@@ -2913,6 +2974,7 @@ const void* trace_kernel_symbol(int flags) {
         K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15)
         K(F_ALL | F_PROJ) K(F_ALL | F_PROJ | F_TEX)
         K(64) K(65) K(66) K(67) K(68) K(69) K(70) K(71) K(72) K(73) K(74) K(75) K(76) K(77) K(78) K(79)
+        K(129) K(131) K(133) K(135) K(137) K(139) K(141) K(143)
 #undef K
     }
     return nullptr;
@@ -2933,6 +2995,7 @@ hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const Wo
         K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15)
         K(F_ALL | F_PROJ) K(F_ALL | F_PROJ | F_TEX)
         K(64) K(65) K(66) K(67) K(68) K(69) K(70) K(71) K(72) K(73) K(74) K(75) K(76) K(77) K(78) K(79)
+        K(129) K(131) K(133) K(135) K(137) K(139) K(141) K(143)
 #undef K
     default:
         return hipErrorInvalidValue;

@@ -66,12 +66,23 @@ def shard(rank, world, samples, split):
     raise ValueError("split must be 'sample' or 'tile', got %r" % (split,))
 
 
-def tile_owner_mask(width, height, tile_stride, tile_offset):
+def diagonal_ownership(width, tile_stride, mesh_affine):
+    """Whether libptmi splits tiles diagonally (ptmi_api.cpp ptmi_scene_render): affine mesh
+    scenes whose tile rows divide by the stride; raster striding otherwise."""
+    tx = (width + TILE - 1) // TILE
+    return bool(mesh_affine) and tile_stride > 1 and tx % tile_stride == 0
+
+
+def tile_owner_mask(width, height, tile_stride, tile_offset, diagonal=False):
     """Boolean (H, W) mask of the pixels a tile-split rank owns: tiles are 8x8,
-    numbered row-major over ceil(W/8) x ceil(H/8) (the kernel's tile index)."""
+    numbered row-major over ceil(W/8) x ceil(H/8) (the kernel's tile index); rank
+    tile_offset owns tile t when t mod tile_stride == tile_offset (raster), or tile
+    (x, y) when (x + y) mod tile_stride == tile_offset (diagonal, diagonal_ownership)."""
     import numpy as np
     tx = (width + TILE - 1) // TILE
     ys, xs = np.mgrid[0:height, 0:width]
+    if diagonal:
+        return ((ys // TILE + xs // TILE) % tile_stride) == tile_offset
     tile = (ys // TILE) * tx + xs // TILE
     return (tile % tile_stride) == tile_offset
 

@@ -36,13 +36,25 @@ def test_sample_shards_partition(world, samples):
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 @pytest.mark.parametrize("w,h", [(1280, 960), (37, 23), (8, 8)])
-def test_tile_shards_partition(world, w, h):
+@pytest.mark.parametrize("mesh", [False, True])
+def test_tile_shards_partition(world, w, h, mesh):
+    """Raster and diagonal ownership both partition the frame; the diagonal one (mesh
+    scenes whose tile rows divide by the rank count) gives every rank the same number of
+    tiles in every tile row and every tile column."""
+    diag = pdist.diagonal_ownership(w, world, mesh)
     cover = np.zeros((h, w), dtype=np.int64)
     for r in range(world):
         s0, s1, ts, to = pdist.shard(r, world, 7, "tile")
         assert (s0, s1, ts) == (0, 7, world)
-        cover += pdist.tile_owner_mask(w, h, ts, to)
+        m = pdist.tile_owner_mask(w, h, ts, to, diag)
+        cover += m
+        if diag:
+            tiles = m[::8, ::8]
+            assert (tiles.sum(axis=1) == tiles.shape[1] // world).all()
+            if tiles.shape[0] % world == 0:
+                assert (tiles.sum(axis=0) == tiles.shape[0] // world).all()
     assert (cover == 1).all()
+    assert diag == (mesh and world > 1 and ((w + 7) // 8) % world == 0)
 
 
 def test_shard_rejects_bad_arguments():

@@ -88,9 +88,10 @@ def test_full_frame_matches_live_reference(cfg, scene, ap, fl):
 
 @pytest.mark.parametrize("scene,ap,fl,split", [("reference", 0.15, 1.6, "sample"), ("gopher", 0.0, 0.0, "tile")])
 def test_eight_gpu_shards_sum_to_frame_at_full_resolution(scene, ap, fl, split):
-    """The shards 8 ranks render (C3: cost-balanced sample ranges; C5: 8x8 tiles
-    round-robin) summed in rank order equal the one-GPU frame: bit-identical for the
-    tile split, FP64 summation order for the sample split."""
+    """The shards 8 ranks render (C3: cost-balanced sample ranges; C5: 8x8 tiles, owned
+    diagonally -- 160 tiles per row divide by 8, ptmi_api.cpp render) summed in rank order
+    equal the one-GPU frame: bit-identical for the tile split, FP64 summation order for the
+    sample split."""
     import torch
     W, H, S, world = 1280, 960, 48, 8
     objs, tris, grps, cam = scene_inputs(scene, W, H, ap, fl)

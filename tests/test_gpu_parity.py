@@ -236,6 +236,34 @@ def test_tile_split_partitions_frame():
     assert torch.equal(acc, full)
 
 
+@pytest.mark.parametrize("scene,stride", [("teapot", 4), ("gopher", 8), ("teapot", 3)])
+def test_mesh_tile_split_ownership(scene, stride):
+    """Tile split of an affine mesh scene (ptmi_api.cpp render): diagonal ownership through
+    the F_TLIST kernels when the tile rows divide by the stride (16 tiles per row: 4 and 8),
+    raster striding otherwise (3).  Each rank's frame holds exactly its tiles (A = S there,
+    zeros elsewhere, as ptmi/dist.py's tile_owner_mask predicts) and the shards sum to the
+    one-launch frame."""
+    from ptmi import dist as pdist
+    W, H, S = 128, 48, 24
+    torch, sc = _torch_scene(scene, W, H)
+    seeds = torch.tensor(layout.seeds_go_float64(W * H, 12), dtype=torch.float64, device="cuda")
+    full = torch.empty(W * H * 4, dtype=torch.float64, device="cuda")
+    sc.render(S, 0, S, seeds.data_ptr(), full.data_ptr(), chunks=3)
+    acc = torch.zeros_like(full)
+    part = torch.empty_like(full)
+    diag = pdist.diagonal_ownership(W, stride, True)
+    assert diag == (stride != 3)
+    for g in range(stride):
+        sc.render(S, 0, S, seeds.data_ptr(), part.data_ptr(), tile_stride=stride, tile_offset=g, chunks=3)
+        torch.cuda.synchronize()
+        mask = torch.tensor(pdist.tile_owner_mask(W, H, stride, g, diag).reshape(-1), device="cuda")
+        p4 = part.view(-1, 4)
+        assert torch.all(p4[mask, 3] == S) and torch.all(p4[~mask] == 0)
+        acc += part
+    assert torch.equal(acc, full)  # same chunks per tile in every launch: bit for bit
+    sc.close()
+
+
 def test_errors_are_loud():
     objs, tris, grps, cam = scene_inputs("reference", 8, 8)
     with pytest.raises(api.PtmiError) as e:

@@ -13,8 +13,10 @@ if [ "$NAME" = head ] || [ -n "$FROMREV" ]; then
   for f in ptmi_kernels.hip ptmi_api.cpp ptmi_bvh.cpp ptmi_bvh.h ptmi_device.h ptmi_sinf.h ptmi_fp64core.h ptmi_f16.h; do
     git show $REV:pathtracer-ocl_amd/csrc/$f > $SRC/$f
   done
-  cp -r ../include $(dirname $SRC)/../include 2>/dev/null || true
-  git show $REV:include/ptmi.h > $(dirname $SRC)/../include/ptmi.h
+  mkdir -p $(dirname $SRC)/../include
+  for f in ptmi.h ptmi_diag.h ptmi_host.h; do
+    git show $REV:include/$f > $(dirname $SRC)/../include/$f 2>/dev/null || true
+  done
 fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wno-unused-result \
   "$@" -shared -o build/exp/libptmi_$NAME.so $SRC/ptmi_kernels.hip $SRC/ptmi_api.cpp $SRC/ptmi_bvh.cpp

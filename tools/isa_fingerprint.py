@@ -44,7 +44,11 @@ def fingerprints(asm):
         # (labels past the first s_endpgm are not in `names`: drop the function number)
         norm = [re.sub(r"\.LBB\d+_(\d+)", lambda x: names.get(x.group(0), ".LBB_" + x.group(1)), t) for t in ins]
         h = hashlib.sha256("\n".join(norm).encode()).hexdigest()[:16]
-        res[fl] = (len(ins), h)
+        # the same with kernel-argument offsets masked (a field appended to a by-value argument
+        # struct moves the later arguments' offsets and nothing else)
+        ka = [re.sub(r"(s\[0:1\]), 0x[0-9a-f]+", r"\1, KA", t) for t in norm]
+        hk = hashlib.sha256("\n".join(ka).encode()).hexdigest()[:16]
+        res[fl] = (len(ins), h, hk)
     # resource usage from the metadata block (one entry per kernel, in .amdgpu_metadata)
     meta = {}
     for mm in re.finditer(r"\.name:\s+(_ZN4ptmi12trace_kernelILi(\d+)EEEv\w*)", asm):
@@ -59,6 +63,6 @@ def fingerprints(asm):
 if __name__ == "__main__":
     res, meta = fingerprints(device_asm(sys.argv[1:]))
     for fl in sorted(res):
-        n, h = res[fl]
+        n, h, hk = res[fl]
         vg, sc = meta.get(fl, ("?", "?"))
-        print("trace_kernel<%-2d> insts %6d  vgpr %-4s scratch %-4s isa %s" % (fl, n, vg, sc, h))
+        print("trace_kernel<%-3d> insts %6d  vgpr %-4s scratch %-4s isa %s  isa-ka %s" % (fl, n, vg, sc, h, hk))
