@@ -225,10 +225,6 @@ def main():
     ap.add_argument("--split", action="store_true",
                     help="DIAGNOSTIC: mesh scenes in the split form (needs PTMI_LIB=<the study library>)")
     args = ap.parse_args()
-    knobs = []
-    for kv in args.knob:
-        k, v = kv.split("=", 1)
-        knobs.append((getattr(api, "KNOB_" + k.strip().upper()), int(v)))
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -244,6 +240,10 @@ def main():
     import torch.distributed as dist
     from ptmi import api, layout
     from ptmi import dist as pdist
+    knobs = []  # --knob NAME=VALUE (DIAGNOSTIC)
+    for kv in args.knob:
+        k, v = kv.split("=", 1)
+        knobs.append((getattr(api, "KNOB_" + k.strip().upper()), int(v)))
     from tests.scene_inputs import scene_inputs
 
     ndev = torch.cuda.device_count()
