@@ -424,6 +424,18 @@ int32_t finalize_index_codes(RootIndex& idx, std::vector<RootRec>& recs) {
     for (Node4& nd : idx.nodes)
         for (int i = 0; i < 4; i++) nd.child[i] = recode(nd.child[i]);
     for (RootRec& r : recs) r.entry = recode(r.entry);
+#if defined(PTMI_STACKLESS) && PTMI_STACKLESS
+    // DIAGNOSTIC stackless walk (ptmi_kernels.hip walk_index_stackless): each Node4's parent in
+    // the high half of its child[0] (16-bit codes leave it free; 0xFFFF at a root).
+    if (narrow) {
+        std::vector<uint32_t> parent(idx.nodes.size(), 0xFFFFu);
+        for (size_t n = 0; n < idx.nodes.size(); n++)
+            for (int i = 0; i < 4; i++)
+                if (idx.nodes[n].child[i] < lb) parent[idx.nodes[n].child[i]] = (uint32_t)n;
+        for (size_t n = 0; n < idx.nodes.size(); n++)
+            idx.nodes[n].child[0] = (int32_t)(((uint32_t)idx.nodes[n].child[0] & 0xFFFFu) | (parent[n] << 16));
+    }
+#endif
     return lb;
 }
 

@@ -800,7 +800,11 @@ __device__ __forceinline__ bool key_entered(double k) { return __double2hiint(k)
 __device__ __forceinline__ int key_code(double k) { return __double2loint(k); }
 
 // The four child slab tests of Node4 `cur` (one walk step): keys of its children.
-__device__ __forceinline__ void node_children(const DevScene& S, int cur, const WalkRay& W, float lim, double k[4]) {
+#ifndef PTMI_STACKLESS
+#define PTMI_STACKLESS 0  // DIAGNOSTIC (study builds): the stackless walk (walk_index_stackless)
+#endif
+__device__ __forceinline__ void node_children(const DevScene& S, int cur, const WalkRay& W, float lim, double k[4],
+                                              int* parent = nullptr) {
     // The node's 64 B as four 16-B global loads issued together (one wait).  Bounds are
     // binary16 (ptmi_device.h), converted exactly to float inside v_fma_mix_f32, so the
     // slab test is the float-box one; a bound past the binary16 range is +-inf, whose
@@ -822,7 +826,13 @@ __device__ __forceinline__ void node_children(const DevScene& S, int cur, const 
     auto h16 = [](uint32_t w, int i) {
         return (float)__builtin_bit_cast(_Float16, (uint16_t)((i & 1) ? (w >> 16) : (w & 0xffffu)));
     };
+#if PTMI_STACKLESS
+    // (stackless study: child[0]'s high half holds the node's parent, finalize_index_codes)
+    const int ch[4] = {(int)(q[3].x & 0xFFFFu), (int)q[3].y, (int)q[3].z, (int)q[3].w};
+    if (parent) *parent = (int)(q[3].x >> 16);
+#else
     const int ch[4] = {(int)q[3].x, (int)q[3].y, (int)q[3].z, (int)q[3].w};
+#endif
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         float tn = 0.0f, tf = lim;
@@ -929,6 +939,62 @@ __device__ __forceinline__ void walk_index(const DevScene& S, Stk* __restrict__ 
     if (n_steps == 1) PTMI_COUNT(21);
 #endif
 }
+
+#if PTMI_STACKLESS
+// DIAGNOSTIC (study): the stackless form of walk_index that north_star names -- no traversal
+// stack: a walk keeps its node, the key of the child it last left (the next child is the
+// nearest entered one beyond it: child keys order children by (entry distance, code), the
+// order walk_index pushes them in) and, on the way up, the child it came from, whose key it
+// re-derives from the parent's re-tested children.  Each Node4 carries its parent in the
+// high half of child[0] (finalize_index_codes, PTMI_STACKLESS builds).  Every node is re-tested
+// once per child walked into; leaves are visited in the stack walk's order, so the candidates
+// and hence the winner are the same (the pruning limit only shrinks: a child culled on a
+// re-test lies beyond the best hit, and so do its later siblings).
+template <bool kVerify>
+__device__ __forceinline__ void walk_index_stackless(const DevScene& S, const RootRec& R, int slot, int key, d4 o,
+                                                     d4 d, d4 rw, Hit& h, int& vchain) {
+    const WalkRay W = walk_setup(o, rw, R);
+    float lim = walk_limit(h.t);
+    int cur = R.entry;
+    if (cur >= kLeafNarrow) {  // a root that is a single leaf (or empty)
+        leaf_visit<kVerify>(S, cur - kLeafNarrow, slot, key, o, d, h, vchain);
+        return;
+    }
+    const int root = cur;
+    double thr = -__builtin_huge_val();  // children with keys above thr are still to walk
+    int from = -1;                        // the child node walked out of, or -1
+    while (true) {
+        double k[4];
+        int parent;
+        node_children(S, cur, W, lim, k, &parent);
+        if (from >= 0) {  // coming up from child `from`: resume after its key
+            thr = __builtin_huge_val();  // (from culled now: so is every later sibling)
+#pragma unroll
+            for (int i = 0; i < 4; i++) thr = key_code(k[i]) == from ? k[i] : thr;
+        }
+        double nk = __builtin_huge_val();
+#pragma unroll
+        for (int i = 0; i < 4; i++) nk = (key_entered(k[i]) && k[i] > thr) ? fmin(nk, k[i]) : nk;
+        if (nk == __builtin_huge_val()) {  // node exhausted
+            if (cur == root) break;
+            from = cur;
+            cur = parent;
+            continue;
+        }
+        const int c = key_code(nk);
+        if (c < kLeafNarrow) {
+            cur = c;
+            from = -1;
+            thr = -__builtin_huge_val();
+        } else {
+            leaf_visit<kVerify>(S, c - kLeafNarrow, slot, key, o, d, h, vchain);
+            lim = walk_limit(h.t);
+            from = -1;
+            thr = nk;
+        }
+    }
+}
+#endif
 
 // Candidate update as selects (no exec-mask branching).  t > EPSILON implies
 // the reference's `t != 0.0` recording test.
@@ -1267,6 +1333,10 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, Stk* __restr
                          R.hull_mx[2], h.t + prune_margin(h.t), tn))
                 continue;
             PTMI_TSTAMP(t_w);
+#if PTMI_STACKLESS
+            if constexpr (A) walk_index_stackless<kVerify>(S, R, j, ob.key, o, d, r, h, vchain);
+            else
+#endif
             walk_index<kVerify>(S, stk, R, j, ob.key, o, d, r, h, vchain);
             PTMI_TADD_ACTIVE(18, t_w);  // (stats: cycles in walk loops)
         }

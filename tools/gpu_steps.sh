@@ -8,6 +8,7 @@
 #   prof:<cfg>                 rocprofv3 --kernel-trace --stats of bench.py --config <cfg> --extra none
 #   profx:<name>:<lib>:<args>  the same for build/<lib>.so and bench args (comma-separated), e.g. the split form
 #   pmc:<cfg>:<counters>       one rocprofv3 --pmc pass (counters comma-separated) of the same
+#   pmcx:<name>:<lib>:<ctrs>:<args>  one --pmc pass of any bench command with build/<lib>.so
 #   shards:<cfgs>:<worlds>     tools/shard_balance.py (comma-separated lists)
 set -o pipefail
 OUT=gpurun_out/$1; shift
@@ -43,6 +44,11 @@ for step in "$@"; do
       timeout -s KILL 300 rocprofv3 --pmc ${b//,/ } --output-format csv -d $OUT/pmc_${a}_${b//,/_} -o run -- python3 bench.py --config $a \
         --steps 1 --warmup 1 --extra none --no-cpu-baseline --no-trace-call > /dev/null 2> $OUT/pmc_$a.err \
         || { tail -20 $OUT/pmc_$a.err; exit 1; } ;;
+    pmcx)  # pmcx:<name>:<lib>:<counters>:<bench args>, all comma-separated lists
+      IFS=: read -r kind a b c d <<< "$step"
+      PTMI_LIB=pathtracer-ocl_amd/build/${b}.so timeout -s KILL 400 rocprofv3 --pmc ${c//,/ } --output-format csv \
+        -d $OUT/pmcx_${a} -o run -- python3 bench.py ${d//,/ } --extra none --no-cpu-baseline --no-trace-call \
+        > $OUT/pmcx_$a.json 2> $OUT/pmcx_$a.err || { tail -20 $OUT/pmcx_$a.err; exit 1; } ;;
     shards)  # shards:<configs>:<worlds>: every rank's share timed on this GPU (tools/shard_balance.py)
       timeout -k 10 600 python3 tools/shard_balance.py $OUT/shards.json --configs $a --worlds $b > $OUT/shards.log 2>&1 \
         || { tail -20 $OUT/shards.log; exit 1; }
