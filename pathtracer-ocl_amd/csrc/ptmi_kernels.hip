@@ -2018,13 +2018,32 @@ __device__ __forceinline__ void store_sums(const Item& it, const WorkPlan& WP, d
 // rays that reach a mesh in any one bounce.  Each lane still traces its samples in
 // order, and the closest hit does not depend on when or in which order candidates are
 // examined (lexicographic minimum, better()).
+// The scene record through an opaque uniform pointer to the kernel's arguments (DevScene is
+// trace_kernel's first argument): inside the bounce loop its fields are scalar-loaded where
+// they are used instead of being held in SGPRs across the loop (camera_ptr's reasoning).
+#ifndef PTMI_SCENE_RELOAD
+#define PTMI_SCENE_RELOAD 0  // 1: mesh kernels, 2: kernels without meshes, 3: both
+#endif
+template <bool kReload>
+__device__ __forceinline__ const DevScene& scene_reload(const DevScene& S) {
+    if constexpr (!kReload) return S;
+    typedef const __attribute__((address_space(4))) DevScene ConstScene;
+    const DevScene* p = (const DevScene*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm("" : "+s"(p));
+    const uint64_t a = (uint64_t)p;
+    const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32);
+    return *(const DevScene*)(ConstScene*)u;
+}
+
 template <int FL>
-__device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples, const WorkPlan& WP,
+__device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t samples, const WorkPlan& WP,
                                              const double* __restrict__ seeds, const double* __restrict__ sunf,
                                              double* __restrict__ sums, double* __restrict__ part) {
     constexpr bool A = !(FL & F_PROJ);
     constexpr bool kDof = (FL & F_DOF) != 0;
     constexpr int kCamComp = (kDof || !A) ? (A ? 6 : 8) : 3;  // see trace_kernel
+    const DevScene& S = S0;
     // Per-lane BVH traversal stacks, lane-interleaved (entry k of lane t at
     // [k * kStkStride + t]) so a wave's pushes and pops hit 64 consecutive dwords; the
     // per-pixel colour sums (the same additions in the same order) and a parked lane's
@@ -2077,6 +2096,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S, uint32_t samples
     PTMI_TSTAMP(t_loop);
     for (;;) {
         if (!__any(active || buffered || n_gen < c_end)) break;
+        const DevScene& S = scene_reload<(PTMI_SCENE_RELOAD & 1) != 0>(S0);
         PTMI_TSTAMP(t_a);
         // Camera rays in wave-wide batches (see trace_kernel).
         const bool need = !buffered && n_gen < c_end;
@@ -2302,8 +2322,10 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
         bool buffered = false, active = false;
         PathState P;
         PTMI_TSTAMP(t_loop);
+        const DevScene& S0 = S;
         for (;;) {
             if (!__any(active || buffered || n_gen < c_end)) break;
+            const DevScene& S = scene_reload<(PTMI_SCENE_RELOAD & 2) != 0>(S0);
             PTMI_TSTAMP(t_a);
             const bool need = !buffered && n_gen < c_end;
             const int n_need = __popcll(__ballot(need));
@@ -2549,7 +2571,8 @@ __global__ __launch_bounds__(kBlock, PTMI_WALK_WAVES) void walk_pool_kernel(DevS
 // chunk sums go to the same partial records as the mesh kernel's chunk items, so the frame
 // equals a mesh-kernel render with the same chunk length bit for bit.
 #ifndef PTMI_WAVES_SPLIT
-#define PTMI_WAVES_SPLIT 5
+#define PTMI_WAVES_SPLIT 4  // (round 5: 5 waves spilled 208 B/lane, the tracer pass then waited on memory 82 % of
+                            // its cycles; 4: 64 B/lane, C4 split frame 2444 -> 1511 ms, profiles/r5/split)
 #endif
 #ifndef PTMI_SPLIT_BATCH
 #define PTMI_SPLIT_BATCH 16  // waiting lanes that trigger a batched slot / claim / camera step

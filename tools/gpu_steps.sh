@@ -10,6 +10,7 @@
 #   pmc:<cfg>:<counters>       one rocprofv3 --pmc pass (counters comma-separated) of the same
 #   pmcx:<name>:<lib>:<ctrs>:<args>  one --pmc pass of any bench command with build/<lib>.so
 #   shards:<cfgs>:<worlds>     tools/shard_balance.py (comma-separated lists)
+#   shardsk:<tag>:<cfgs>:<worlds>:<knobs>  the same with work-plan knobs (NAME=VALUE, comma-separated)
 set -o pipefail
 OUT=gpurun_out/$1; shift
 mkdir -p $OUT
@@ -53,6 +54,12 @@ for step in "$@"; do
       timeout -k 10 600 python3 tools/shard_balance.py $OUT/shards.json --configs $a --worlds $b > $OUT/shards.log 2>&1 \
         || { tail -20 $OUT/shards.log; exit 1; }
       tail -12 $OUT/shards.log ;;
+    shardsk)  # shardsk:<tag>:<cfgs>:<worlds>:<knobs, comma-separated NAME=VALUE>
+      IFS=: read -r kind a b c d <<< "$step"
+      kn=""; for kv in ${d//,/ }; do kn="$kn --knob $kv"; done
+      timeout -k 10 600 python3 tools/shard_balance.py $OUT/shards_$a.json --configs $b --worlds $c $kn \
+        > $OUT/shards_$a.log 2>&1 || { tail -20 $OUT/shards_$a.log; exit 1; }
+      grep -E "^c[0-9] " $OUT/shards_$a.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -30,13 +30,18 @@ ap.add_argument("out", nargs="?", default="")
 ap.add_argument("--configs", default="c2,c3,c4,c5")
 ap.add_argument("--worlds", default="2,4,8")
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
+                help="a work-plan knob of every scene (ptmi_diag_set_knob), as bench.py --knob")
 a = ap.parse_args()
+knobs = [(getattr(api, "KNOB_" + kv.split("=")[0].strip().upper()), int(kv.split("=")[1])) for kv in a.knob]
 XGMI_GBS = 153.0
-res = {"what": __doc__.strip().splitlines()[0], "device": api.device_name(0), "configs": {}}
+res = {"what": __doc__.strip().splitlines()[0], "device": api.device_name(0), "knobs": a.knob, "configs": {}}
 for cfg in a.configs.split(","):
     scene_name, W, H, S, aper, focal, split, _, desc = bench.CONFIGS[cfg]
     objs, tris, grps, cam = scene_inputs(scene_name, W, H, aper, focal)
     scene = api.Scene(0, objs, tris, grps, cam)
+    for k, v in knobs:
+        assert scene.set_knob(k, v) == api.PTMI_OK, (k, v)
     seeds = torch.tensor(layout.seeds_go_float64(W * H, 1234), dtype=torch.float64, device="cuda")
     sums = torch.empty(W * H * 4, dtype=torch.float64, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
