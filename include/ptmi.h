@@ -216,8 +216,10 @@ const char* ptmi_build_info(void);
  *   decoded child box's surface area, in object-space units  [3] infinite bounds among
  *   them  [4] largest root scale exponent s (bounds stored as (b - ctr) / 2^s)
  *   [5] roots  [6] longest chain of Node4s (the walk's stack holds <= 3 entries per
- *   level; ptmi_bvh.cpp keeps it <= 7).  Index quality (box inflation from the binary16 bounds) can be compared
- *   across translated or scaled copies of one mesh. */
+ *   level; ptmi_bvh.cpp keeps it <= 7)  [7] the child codes' leaf bit: 2^15 when every
+ *   code fits the affine kernels' 16-bit traversal stack, else 2^30 (the scene then runs
+ *   the generic instantiation, 32-bit stack).  Index quality (box inflation from the
+ *   binary16 bounds) can be compared across translated or scaled copies of one mesh. */
 int ptmi_index_stats(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
                      const void* groups, uint32_t n_grp, const void* camera, double* out, int n_out,
                      char* err, size_t err_len);

@@ -798,7 +798,8 @@ int ptmi_index_stats(const void* objects, uint32_t n_obj, const void* triangles,
     HostScene hs;
     int rc = prepare_scene(objects, n_obj, triangles, n_tri, groups, n_grp, camera, nullptr, hs, err, err_len);
     if (rc) return rc;
-    double st[7] = {(double)hs.index.nodes.size(), 0.0, 0.0, 0.0, 0.0, (double)hs.root_rec.size(), 0.0};
+    double st[8] = {(double)hs.index.nodes.size(), 0.0, 0.0, 0.0, 0.0, (double)hs.root_rec.size(), 0.0,
+                    (double)hs.leaf_bit};
     for (const RootRec& R : hs.root_rec) {
         st[4] = std::max(st[4], std::log2((double)R.sc));
         std::vector<std::pair<int32_t, int>> todo;  // (Node4, its level)
@@ -823,7 +824,7 @@ int ptmi_index_stats(const void* objects, uint32_t n_obj, const void* triangles,
             }
         }
     }
-    for (int i = 0; i < n_out && i < 7; i++) out[i] = st[i];
+    for (int i = 0; i < n_out && i < 8; i++) out[i] = st[i];
     return PTMI_OK;
 }
 

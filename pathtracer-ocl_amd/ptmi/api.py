@@ -222,11 +222,12 @@ def index_stats(objects, triangles, groups, camera):
     """ptmi_index_stats (host only): summary of the traversal index the library builds
     for these records -- {nodes4, slots, box_area, inf_bounds, max_scale_exp, roots, depth}."""
     objects, triangles, groups, camera = _records(objects, triangles, groups, camera)
-    out = (ctypes.c_double * 7)()
+    out = (ctypes.c_double * 8)()
     err = ctypes.create_string_buffer(1024)
     _check(load_library().ptmi_index_stats(_ptr(objects), len(objects), _ptr(triangles), len(triangles),
-                                           _ptr(groups), len(groups), _ptr(camera), out, 7, err, len(err)), err)
-    return dict(zip(("nodes4", "slots", "box_area", "inf_bounds", "max_scale_exp", "roots", "depth"), list(out)))
+                                           _ptr(groups), len(groups), _ptr(camera), out, 8, err, len(err)), err)
+    return dict(zip(("nodes4", "slots", "box_area", "inf_bounds", "max_scale_exp", "roots", "depth", "leaf_bit"),
+                    list(out)))
 
 
 class force_flags:

@@ -295,6 +295,24 @@ def test_hip_matches_live_reference_adversarial_bvh(kind, ap):
     assert err < 1e-12, "%s: L-inf %.3e vs live reference" % (kind, err)
 
 
+def test_hip_matches_live_reference_wide_child_codes():
+    """A mesh past 16-bit child codes (tests/adversarial.py "big", 34,848 triangles) takes
+    the wide codes and the generic instantiation's 32-bit traversal stack: still the
+    reference's image."""
+    if not pyoracle.ref_available():
+        pytest.skip("oracle/_ref not built")
+    from tests import adversarial
+    w, h, spp = 64, 48, 2
+    objs, tris, grps, cam = adversarial.scene_inputs("big", w, h)
+    assert api.index_stats(objs, tris, grps, cam)["leaf_bit"] == 0x40000000
+    seeds = layout.seeds_go_float64(w * h, 404)
+    t2, g2 = layout.pad_empty(tris, grps)
+    ref = pyoracle.ref_trace(objs, t2, g2, cam, spp, seeds)
+    out = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    err = np.abs(out - ref).max()
+    assert err < 1e-12, "big: L-inf %.3e vs live reference" % err
+
+
 @pytest.mark.parametrize("offset,scale", [((1.0e4, 0.0, 0.0), 1.0), ((-3.0e4, 2.0e4, 7.5e3), 1.0),
                                           ((1.0e9, 0.0, -2.0e9), 3.0e5)])
 def test_hip_matches_live_reference_moved_mesh(offset, scale):

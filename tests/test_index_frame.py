@@ -106,3 +106,17 @@ def test_tile_classes_are_zero_without_meshes():
     w, h = 64, 48
     objs, tris, grps, cam = scene_inputs("reference", w, h)
     assert _tile_cost(objs, tris, grps, cam, w, h).max() == 0
+
+
+def test_child_codes_narrow_for_the_baseline_meshes(teapot):
+    """Teapot and gopher child codes fit 16 bits: the affine kernels' LDS stack holds them
+    (ptmi_bvh.cpp finalize_index_codes)."""
+    assert _stats(*teapot)["leaf_bit"] == 0x8000
+    assert _stats(*scene_inputs("gopher", 32, 24))["leaf_bit"] == 0x8000
+
+
+def test_child_codes_wide_past_16_bits():
+    """34,848 triangles do not fit 15-bit triangle indices: wide codes (leaf bit 2^30)."""
+    from tests import adversarial
+    st = _stats(*adversarial.scene_inputs("big", 16, 12))
+    assert st["leaf_bit"] == 0x40000000 and st["depth"] <= 7
