@@ -1,4 +1,4 @@
-"""Summarise a tools/profile_round.sh output directory into profiles/<round>/:
+"""Summarise a tools/profile_final.sh output directory into profiles/<round>/:
 kernel_stats_<cfg>.csv, bench_<cfg>.json, pmc_c2*.{csv,json} and SUMMARY.md, plus
 the derived VALU metrics of tools/pmc.sh output directories given as cfg=dir.
     python tools/profile_summary.py gpurun_out/prof_r1b profiles/r1 [c2=gpurun_out/pmc_c2 ...]
@@ -37,7 +37,7 @@ CMDS = {"c2": "python3 bench.py --config c2 --steps 2 --warmup 1",
 
 def main(src, dst, pmc_dirs=()):
     os.makedirs(dst, exist_ok=True)
-    lines = ["# rocprofv3 --kernel-trace --stats summaries (tools/profile_round.sh, one MI355X)", ""]
+    lines = ["# rocprofv3 --kernel-trace --stats summaries (tools/profile_final.sh, one MI355X)", ""]
     for c, cmd in CMDS.items():
         shutil.copy(os.path.join(src, c, "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats_%s.csv" % c))
         shutil.copy(os.path.join(src, "bench_%s.json" % c), os.path.join(dst, "bench_%s.json" % c))
