@@ -56,8 +56,17 @@ enum {
 static __thread uint64_t g_ev[EV_COUNT];
 static uint64_t g_ev_total[EV_COUNT];
 #define CNT(e) (g_ev[(e)]++)
+/* The reference's ctx entries of one findClosestIntersection call (every candidate it
+ * records, t != 0, negative t included; tracer.cl:553-672) and their maximum over a trace:
+ * its ctx arrays hold 64 (tracer.cl:97-99), so a scene whose maximum exceeds 64 overflows
+ * them in the reference (undefined behaviour) and cannot be a live-reference
+ * parity case. */
+static __thread int g_xs, g_xs_max;
+static int g_xs_max_total;
+#define XS_RECORD() (g_xs++)
 #else
 #define CNT(e) ((void)0)
+#define XS_RECORD() ((void)0)
 #endif
 
 #define MAX_EFFECTIVE_BOUNCES 4u /* tracer.cl:2 */
@@ -357,6 +366,7 @@ typedef struct {
 } hit_t;
 
 static inline void consider(hit_t* h, double t, int obj, int tri, double u, double v) {
+    XS_RECORD();
     if (t > EPSILON && t < h->t) {
         h->t = t;
         h->obj = obj;
@@ -367,7 +377,18 @@ static inline void consider(hit_t* h, double t, int obj, int tri, double u, doub
 }
 
 /* findClosestIntersection (tracer.cl:537-742). */
+static hit_t find_closest_(const scene_t* S, d4 ro, d4 rd);
 static hit_t find_closest(const scene_t* S, d4 ro, d4 rd) {
+#ifdef PTO_COUNT
+    g_xs = 0;
+    const hit_t h = find_closest_(S, ro, rd);
+    if (g_xs > g_xs_max) g_xs_max = g_xs;
+    return h;
+#else
+    return find_closest_(S, ro, rd);
+#endif
+}
+static hit_t find_closest_(const scene_t* S, d4 ro, d4 rd) {
     hit_t h = {1024.0, -1, -1, 0.0, 0.0};
     for (uint32_t j = 0; j < S->n_obj; j++) {
         const object_t* ob = &S->objects[j];
@@ -777,9 +798,11 @@ int pto_trace_tex(const void* objects, uint32_t n_obj, const void* tris, uint32_
 #endif
 #ifdef PTO_COUNT
         memset(g_ev_total, 0, sizeof g_ev_total);
+        g_xs_max_total = 0;
 #pragma omp parallel
         {
             memset(g_ev, 0, sizeof g_ev);
+            g_xs_max = 0;
 #pragma omp for schedule(dynamic, 16)
             for (long p = 0; p < npx; p++) {
                 uint32_t i = row0 * W + (uint32_t)p;
@@ -791,7 +814,10 @@ int pto_trace_tex(const void* objects, uint32_t n_obj, const void* tris, uint32_
                 o[3] = full ? 1.0 : (double)(s1 - s0);
             }
 #pragma omp critical
-            for (int e = 0; e < EV_COUNT; e++) g_ev_total[e] += g_ev[e];
+            {
+                for (int e = 0; e < EV_COUNT; e++) g_ev_total[e] += g_ev[e];
+                if (g_xs_max > g_xs_max_total) g_xs_max_total = g_xs_max;
+            }
         }
 #else
 #pragma omp parallel for schedule(dynamic, 16)
@@ -852,6 +878,15 @@ int pto_event_counts(uint64_t* out, int n) {
     (void)out;
     (void)n;
     return 0;
+#endif
+}
+/* The most ctx entries one findClosestIntersection call of the last pto_trace recorded
+ * (PTO_COUNT build; else -1). */
+int pto_max_candidates(void) {
+#ifdef PTO_COUNT
+    return g_xs_max_total;
+#else
+    return -1;
 #endif
 }
 float pto_sinf32(float x) { return pto_sinf(x); }

@@ -163,6 +163,34 @@ def cpu_trace(objects, triangles, groups, camera, samples, seeds, row0=0, rows=N
     return out
 
 
+def max_candidates(objects, triangles, groups, camera, samples, seeds, row0=0, rows=None):
+    """The most entries the reference would record in its 64-entry ctx arrays
+    (tracer.cl:97-99) in one findClosestIntersection call of this trace: every
+    candidate with t != 0, negative t included (the oracle's counting build, which
+    streams them).  A scene past 64 overflows the reference's arrays (undefined
+    behaviour; the live reference kernel faults on such scenes), so it can be checked
+    against this restatement only."""
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(CPU_LIB), "libptoracle_count.so"))
+    lib.pto_trace.restype = ctypes.c_int
+    lib.pto_trace.argtypes = _cpu_lib().pto_trace.argtypes
+    lib.pto_max_candidates.restype = ctypes.c_int
+    cam = np.asarray(camera).reshape(())
+    w, h = int(cam["width"]), int(cam["height"])
+    rows = h - row0 if rows is None else rows
+    seeds = np.ascontiguousarray(seeds, dtype=np.float64)
+    out = np.zeros(w * rows * 4, dtype=np.float64)
+    objects, po = _as_bytes_ptr(objects)
+    triangles, pt = _as_bytes_ptr(triangles)
+    groups, pg = _as_bytes_ptr(groups)
+    cam_arr, pc = _as_bytes_ptr(cam)
+    rc = lib.pto_trace(po, len(objects), pt, len(triangles), pg, len(groups), pc, samples,
+                       seeds.ctypes.data_as(ctypes.c_void_p), row0, rows, 0, samples, 0,
+                       out.ctypes.data_as(ctypes.c_void_p))
+    if rc != 0:
+        raise RuntimeError("pto_trace rc=%d" % rc)
+    return int(lib.pto_max_candidates())
+
+
 def ray_box(origin, direction, bb_min, bb_max):
     """intersectRayWithBox (tracer.cl:270-280): origin/direction 4-tuples, box corners 3-tuples."""
     a = [np.ascontiguousarray(v, dtype=np.float64) for v in (origin, direction, bb_min, bb_max)]

@@ -1438,8 +1438,9 @@ __device__ __forceinline__ void hemi_sqrt(float u2, double& r2s, double& rc) {
 // and ptmi_diag_hemi_mismatch reports the count, 0 on this toolchain).  Off-grid draws
 // compute; the statistical mode draws its hemisphere uniforms on the grid (xnext16).
 #ifndef PTMI_HEMI_TAB_GROUPS
-#define PTMI_HEMI_TAB_GROUPS 0  // mesh scenes compute: the 2 MB table competes with the BVH for the 4 MB
-                                // L2 of an XCD (512 spp: C5 264 vs 268-269 ms with it, C4 170.6 vs 170.2)
+#define PTMI_HEMI_TAB_GROUPS 1  // mesh scenes read the table too (round 5: with the group kernel's colour
+                                // state in LDS, 2048 spp: C4 594 -> 577, C5 902 -> 897 ms; in round 4 the
+                                // 2 MB table's L2 share had cost C5 ~1.5 % at 512 spp)
 #endif
 static constexpr int kHemiBits = 16;
 static constexpr int kHemiSize = 1 << kHemiBits;
@@ -2010,19 +2011,14 @@ __device__ __forceinline__ void store_sums(const Item& it, const WorkPlan& WP, d
     o[3] = (double)(it.c1 > it.c0 ? it.c1 - it.c0 : 0);
 }
 
-// trace_kernel's body for scenes with BVH groups: the loop of the other scenes, with
-// the BVH walks deferred.  A lane whose ray needs a walk (group_needs_walk) parks
-// (pending, keeping its primitives' best in LDS) and the wave walks all parked lanes
-// together once kWalkBatch are parked or no lane is ready to shade -- a walk costs the
-// whole wave its longest traversal, so it should run with many lanes, not the ~10 % of
-// rays that reach a mesh in any one bounce.  Each lane still traces its samples in
-// order, and the closest hit does not depend on when or in which order candidates are
-// examined (lexicographic minimum, better()).
 // The scene record through an opaque uniform pointer to the kernel's arguments (DevScene is
 // trace_kernel's first argument): inside the bounce loop its fields are scalar-loaded where
-// they are used instead of being held in SGPRs across the loop (camera_ptr's reasoning).
+// they are used instead of being held in SGPRs across the loop (camera_ptr's reasoning):
+// fewer SGPRs live across the loop, fewer of them spilled to VGPR lanes (the C2 loop's
+// static v_readlane count 32 -> 18).  2048 spp, one MI355X (profiles/r5/SUMMARY.md s6):
+// C3 158.4 -> 156.3 ms; with PTMI_HEMI_TAB_GROUPS C4 577 -> 561, C5 897 -> 882 ms; C2 unchanged.
 #ifndef PTMI_SCENE_RELOAD
-#define PTMI_SCENE_RELOAD 0  // 1: mesh kernels, 2: kernels without meshes, 3: both
+#define PTMI_SCENE_RELOAD 3  // 1: mesh kernels, 2: kernels without meshes, 3: both (0: off)
 #endif
 template <bool kReload>
 __device__ __forceinline__ const DevScene& scene_reload(const DevScene& S) {
@@ -2036,6 +2032,14 @@ __device__ __forceinline__ const DevScene& scene_reload(const DevScene& S) {
     return *(const DevScene*)(ConstScene*)u;
 }
 
+// trace_kernel's body for scenes with BVH groups: the loop of the other scenes, with
+// the BVH walks deferred.  A lane whose ray needs a walk (group_needs_walk) parks
+// (pending, keeping its primitives' best in LDS) and the wave walks all parked lanes
+// together once kWalkBatch are parked or no lane is ready to shade -- a walk costs the
+// whole wave its longest traversal, so it should run with many lanes, not the ~10 % of
+// rays that reach a mesh in any one bounce.  Each lane still traces its samples in
+// order, and the closest hit does not depend on when or in which order candidates are
+// examined (lexicographic minimum, better()).
 template <int FL>
 __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t samples, const WorkPlan& WP,
                                              const double* __restrict__ seeds, const double* __restrict__ sunf,

@@ -14,9 +14,13 @@ They target the exactness arguments of the BVH path:
   * "far"    -- "stairs" plus two small grids at x = +-1e5, past binary16's
                 range: the traversal boxes above them carry +-infinity bounds
                 (ptmi_bvh.cpp), which must stay conservative;
-  * "big"    -- a 34,848-triangle height field: more triangles than 16-bit child
-                codes address, so the scene takes the wide codes and the generic
-                instantiation with its 32-bit traversal stack.
+  * "big"    -- a 34,848-triangle tilted planar grid: more triangles than 16-bit
+                child codes address, so the scene takes the wide codes and the generic
+                instantiation with its 32-bit traversal stack;
+  * "bumpy"  -- the same grid as a bumpy height field: lines along it meet up to ~200
+                triangles, past the reference's 64-entry ctx arrays (tracer.cl:97-99;
+                its kernel faults on this scene), so it is checked against the oracle
+                only (pyoracle.max_candidates names the limit).
 """
 import os
 import tempfile
@@ -68,13 +72,14 @@ def obj_text(kind):
                 for i in range(4):
                     a = base + j * 5 + i + 1
                     faces += [(a, a + 1, a + 6), (a, a + 6, a + 5)]
-    elif kind == "big":  # 34,848 triangles: child codes past 16 bits (the generic kernels' 32-bit stack)
+    elif kind in ("big", "bumpy"):  # 34,848 triangles: child codes past 16 bits (32-bit stack)
         n = 132
         base = len(verts)
         for j in range(n + 1):
             for i in range(n + 1):
                 x, y = -6.0 + 12.0 * i / n, -1.0 + 12.0 * j / n
-                verts.append((x, y, 0.25 * ((i * 7 + j * 13) % 5) / 4.0))  # a bumpy height field
+                z = 0.25 * ((i * 7 + j * 13) % 5) / 4.0 if kind == "bumpy" else 0.05 * y - 0.5
+                verts.append((x, y, z))
         for j in range(n):
             for i in range(n):
                 a = base + j * (n + 1) + i + 1

@@ -289,10 +289,19 @@ def test_hip_matches_live_reference_adversarial_bvh(kind, ap):
     objs, tris, grps, cam = adversarial.scene_inputs(kind, w, h, ap, 1.6 if ap else 0.0)
     seeds = layout.seeds_go_float64(w * h, 300 + len(tris))
     t2, g2 = layout.pad_empty(tris, grps)
+    _assert_ref_defined(objs, t2, g2, cam, spp, seeds)
     ref = pyoracle.ref_trace(objs, t2, g2, cam, spp, seeds)
     out = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
     err = np.abs(out - ref).max()
     assert err < 1e-12, "%s: L-inf %.3e vs live reference" % (kind, err)
+
+
+def _assert_ref_defined(objs, t2, g2, cam, spp, seeds):
+    """A live-reference case must stay inside the reference kernel's 64-entry ctx arrays
+    (tracer.cl:97-99): past them its behaviour is undefined (it faults the GPU).  Checked
+    on the CPU before the reference kernel is launched."""
+    n = pyoracle.max_candidates(objs, t2, g2, cam, spp, seeds)
+    assert 0 < n <= 64, "%d candidates on one line: past the reference's ctx arrays" % n
 
 
 def test_hip_matches_live_reference_wide_child_codes():
@@ -307,10 +316,28 @@ def test_hip_matches_live_reference_wide_child_codes():
     assert api.index_stats(objs, tris, grps, cam)["leaf_bit"] == 0x40000000
     seeds = layout.seeds_go_float64(w * h, 404)
     t2, g2 = layout.pad_empty(tris, grps)
+    _assert_ref_defined(objs, t2, g2, cam, spp, seeds)
     ref = pyoracle.ref_trace(objs, t2, g2, cam, spp, seeds)
     out = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
     err = np.abs(out - ref).max()
     assert err < 1e-12, "big: L-inf %.3e vs live reference" % err
+
+
+def test_hip_matches_oracle_past_reference_ctx():
+    """The bumpy 34,848-triangle height field (tests/adversarial.py "bumpy"): lines along it
+    meet up to ~200 triangles, past the reference's 64-entry ctx arrays, where the reference
+    kernel is undefined (it faults).  ptmi streams the candidates, as the CPU oracle does:
+    the two images agree."""
+    from tests import adversarial
+    w, h, spp = 64, 48, 2
+    objs, tris, grps, cam = adversarial.scene_inputs("bumpy", w, h)
+    seeds = layout.seeds_go_float64(w * h, 404)
+    t2, g2 = layout.pad_empty(tris, grps)
+    assert pyoracle.max_candidates(objs, t2, g2, cam, spp, seeds) > 64
+    ora = pyoracle.cpu_trace(objs, t2, g2, cam, spp, seeds)
+    out = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    err = np.abs(out - ora).max()
+    assert err < 1e-12, "bumpy: L-inf %.3e vs the CPU oracle" % err
 
 
 @pytest.mark.parametrize("offset,scale", [((1.0e4, 0.0, 0.0), 1.0), ((-3.0e4, 2.0e4, 7.5e3), 1.0),

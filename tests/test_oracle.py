@@ -99,3 +99,21 @@ def test_textured_object_without_textures_is_black():
     a = pyoracle.cpu_trace(tex, tris, grps, cam, 2, seeds)
     b = pyoracle.cpu_trace(black, tris, grps, cam, 2, seeds)
     assert np.array_equal(a, b)
+
+
+def test_golden_cases_stay_inside_reference_ctx(golden_cases):
+    """Every golden case records at most 64 candidates per line in the reference's ctx
+    arrays (tracer.cl:97-99), so the reference's image is defined there; the adversarial
+    "bumpy" mesh goes past them (it is an oracle-only case) and "big" does not."""
+    for name, z in golden_cases.items():
+        objs, tris, grps, cam = _inputs(z)
+        seeds = np.asarray(z["seeds"], dtype=np.float64)
+        t2, g2 = layout.pad_empty(tris, grps)
+        n = pyoracle.max_candidates(objs, t2, g2, cam, 1, seeds, rows=4)
+        assert 0 < n <= 64, (name, n)
+    from tests import adversarial
+    for kind, past in (("big", False), ("bumpy", True)):
+        objs, tris, grps, cam = adversarial.scene_inputs(kind, 64, 48)
+        t2, g2 = layout.pad_empty(tris, grps)
+        n = pyoracle.max_candidates(objs, t2, g2, cam, 2, layout.seeds_go_float64(64 * 48, 404))
+        assert (n > 64) == past, (kind, n)
