@@ -38,7 +38,8 @@
 // object tests [8] walk phases [9] lanes in phases [10] wave loop iterations [11] eager
 // re-walks [12..16] shader-clock cycles in refill / closest-prims+gate / walk phases /
 // shade / whole loop [17] exact chain verifications [18] cycles in walk loops
-// [19] wave-level walk loop iterations.
+// [19] wave-level walk loop iterations [27] / [28] (mesh kernels, timers build) lane-cycles
+// of lanes whose work item is finished / all lane-cycles of the loop.
 __device__ unsigned long long ptmi_stats[40];
 // Per-wave accumulators (one writer per wave: the first active lane), flushed to
 // ptmi_stats with one atomic per counter when the wave leaves its loop, so clock
@@ -2224,6 +2225,13 @@ __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t sample
         }
         PTMI_TADD(15, t_d);
         PTMI_WADD(10, 1ull);
+#if PTMI_STATS == 2
+        {  // (timers build: lane-cycles of lanes whose item has no sample left, [27] of [28])
+            const unsigned long long dt = clock64() - t_a;
+            PTMI_WADD(27, dt * (unsigned long long)__popcll(__ballot(!active && !buffered && n_gen >= c_end)));
+            PTMI_WADD(28, dt * 64ull);
+        }
+#endif
     }
     PTMI_TADD(16, t_loop);
 #if PTMI_STATS
