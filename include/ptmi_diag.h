@@ -56,7 +56,9 @@ int ptmi_diag_split_passes(const ptmi_scene* s);
  * MIN_CHUNK: fewest samples per chunk item; TILE_ORDER: dispatch order of a mesh scene's
  * chunked tiles, 0 raster, 1 costliest static class first (default), 2 from the last
  * launch's measured item durations (study build only); SPLIT_*: the split form's pool
- * (study build only).  PTMI_ERR_UNSUPPORTED for a knob or value this build lacks. */
+ * (study build only); TAIL_SPLIT: a mesh scene's automatic plan cuts its last chunk round into
+ * this many shorter rounds (1 = off).  PTMI_ERR_UNSUPPORTED for a knob or value this build
+ * lacks. */
 enum {
     PTMI_KNOB_TAIL_TILES = 1,
     PTMI_KNOB_TAIL_ITEMS = 2,
@@ -66,7 +68,8 @@ enum {
     PTMI_KNOB_SPLIT_CHUNK = 6,
     PTMI_KNOB_SPLIT_SLOTS = 7,
     PTMI_KNOB_SPLIT_SYNC = 8,
-    PTMI_KNOB_SPLIT_BUDGET = 9
+    PTMI_KNOB_SPLIT_BUDGET = 9,
+    PTMI_KNOB_TAIL_SPLIT = 10
 };
 int ptmi_diag_set_knob(ptmi_scene* s, int knob, int value);
 

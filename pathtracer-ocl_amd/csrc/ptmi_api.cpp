@@ -86,6 +86,7 @@ struct ptmi_scene {
     uint32_t tail_items = 6;  // chunk items per resident wave slot in the tail (scenes without meshes; see render)
     uint32_t mesh_items = 32;  // chunk items per resident wave slot, mesh scenes (every tile chunked)
     uint32_t min_chunk = 32;   // fewest samples per chunk item (see render)
+    uint32_t tail_split = 4;   // mesh scenes: the last chunk round cut into this many (see render)
     // Mesh scenes: per-tile cost class (mesh_tile_cost) and the dispatch order built from it
     // for the last (tile_stride, tile_offset) rendered (see render).
     // 0: raster order, 1: static (hull-hit classes), 2: measured by the last launch (needs a
@@ -950,11 +951,14 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         nch = std::max<uint32_t>(1, std::min<uint32_t>(nch, range));
         wp.chunk_len = (range + nch - 1) / nch;
         wp.nchunks = (range + wp.chunk_len - 1) / wp.chunk_len;
+        wp.n_long = wp.nchunks;
+        wp.tail_len = wp.chunk_len;
         wp.n_whole = 0;
         wp.n_tail = owned_tiles;
     }
 #endif
     uint32_t n_tail = owned_tiles;
+    const bool auto_chunks = chunks == 0;
     if (split) {
         chunks = wp.nchunks;
     } else if (chunks == 0) {
@@ -973,6 +977,24 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     wp.n_tail = n_tail;
     wp.nchunks = chunks;
     wp.chunk_len = chunk_len;
+    wp.n_long = chunks;
+    wp.tail_len = chunk_len;
+    // Mesh scenes, automatic plans: the last chunk round is cut into tail_split shorter rounds,
+    // numbered last (and so dispatched last), so the launch drains on short items -- the
+    // end-of-launch ramp was 3.1 % of the one-GPU C5 frame's slot-time (profiles/r4/timeline).
+    // 2048 spp, one MI355X (profiles/r5/tail_split): C5 876 -> 865 ms, C4 unchanged.  Only
+    // while the short chunks keep >= min_chunk / 2 samples: on 8-rank shares (64-sample chunks)
+    // 16-sample ones cost C4's sample split more at each item's end than they saved at the
+    // launch's (projected efficiency 0.893 -> 0.878) and left C5's tile split as it was.
+    // Chunks are summed in chunk order either way.
+    const uint32_t tl = (chunk_len + std::max<uint32_t>(s->tail_split, 1) - 1) / std::max<uint32_t>(s->tail_split, 1);
+    if (!split && auto_chunks && (s->flags & 1) && chunks > 1 && s->tail_split > 1 && tl >= s->min_chunk / 2) {
+        const uint32_t rest = range - (chunks - 1) * chunk_len;
+        wp.n_long = chunks - 1;
+        wp.tail_len = tl;
+        wp.nchunks = wp.n_long + (rest + tl - 1) / tl;
+        chunks = wp.nchunks;
+    }
     wp.order = nullptr;
     wp.cost = nullptr;
     wp.tiles = nullptr;
@@ -1548,6 +1570,7 @@ extern "C" int ptmi_diag_set_knob(ptmi_scene* s, int knob, int value) {
     case PTMI_KNOB_TAIL_ITEMS: s->tail_items = pos; return PTMI_OK;
     case PTMI_KNOB_MESH_ITEMS: s->mesh_items = pos; return PTMI_OK;
     case PTMI_KNOB_MIN_CHUNK: s->min_chunk = pos; return PTMI_OK;
+    case PTMI_KNOB_TAIL_SPLIT: s->tail_split = pos; return PTMI_OK;
     case PTMI_KNOB_TILE_ORDER:
         // 2 (the order measured by the last launch) needs the item timing that only the study
         // build compiles in (ptmi_kernels.hip PTMI_TILE_COST).

@@ -242,6 +242,10 @@ struct WorkPlan {
     uint32_t tile_stride, tile_offset;
     uint32_t n_whole, n_tail;
     uint32_t nchunks, chunk_len;
+    // Chunks [0, n_long) hold chunk_len samples each; the rest (the last rounds of a mesh
+    // scene's automatic plan) hold tail_len each, so the launch ends on short items.
+    // Uniform plans: n_long = nchunks, tail_len = chunk_len.
+    uint32_t n_long, tail_len;
     // Optional dispatch order of the chunked tiles within each chunk round: item tq of a
     // round runs chunked tile order[n_whole + tq] (a permutation of [0, n_tail)); nullptr =
     // identity.  The tile keeps its own partial slot, so the sums and their order do not

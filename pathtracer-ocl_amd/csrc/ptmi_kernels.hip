@@ -1949,6 +1949,12 @@ struct Item {
     uint32_t i;    // pixel index (inside only)
     int px, py;
 };
+// Sample range [c0, c1) of chunk c (WorkPlan::n_long, tail_len).
+__device__ __forceinline__ void chunk_range(const WorkPlan& WP, uint32_t c, uint32_t& c0, uint32_t& c1) {
+    const bool lng = c < WP.n_long;
+    c0 = WP.s_begin + (lng ? c * WP.chunk_len : WP.n_long * WP.chunk_len + (c - WP.n_long) * WP.tail_len);
+    c1 = min(WP.s_end, c0 + (lng ? WP.chunk_len : WP.tail_len));
+}
 // kList (F_TLIST instantiations): owned tile k is WP.tiles[k] (a scalar load of a uniform
 // index) instead of tile_offset + k * tile_stride.
 template <bool kList = false>
@@ -1970,8 +1976,7 @@ __device__ __forceinline__ Item work_item(const DevScene& S, const WorkPlan& WP,
         if (c >= WP.nchunks) return it;
         const uint32_t tt = WP.order ? WP.order[WP.n_whole + tq] : tq;  // the round's tq-th tile in dispatch order
         k = WP.n_whole + tt;
-        it.c0 = WP.s_begin + c * WP.chunk_len;
-        it.c1 = min(WP.s_end, it.c0 + WP.chunk_len);
+        chunk_range(WP, c, it.c0, it.c1);
         it.oslot = ((size_t)c * WP.n_tail + tt) * 64 + lane;
     }
     const uint32_t tile = kList ? WP.tiles[k] : WP.tile_offset + k * WP.tile_stride;
@@ -2992,7 +2997,8 @@ __global__ __launch_bounds__(256) void reduce_chunks_kernel(const double* __rest
             r = r + p[0];
             g = g + p[plane];
             b = b + p[2 * plane];
-            const uint32_t c0 = WP.s_begin + c * WP.chunk_len, c1 = min(WP.s_end, c0 + WP.chunk_len);
+            uint32_t c0, c1;
+            chunk_range(WP, c, c0, c1);
             a = a + (double)(c1 > c0 ? c1 - c0 : 0);  // the chunk item's sample count (work_item)
         } else {
             const double* p = part + ((size_t)c * WP.n_tail * 64 + j) * 4;  // records

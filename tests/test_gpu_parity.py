@@ -197,6 +197,31 @@ def test_sample_split_and_chunking_invariance():
     assert (chunked - full).abs().max().item() < 1e-12
 
 
+def test_mesh_plan_short_last_round():
+    """A mesh scene's automatic plan cuts its last chunk round into shorter chunks
+    (KNOB_TAIL_SPLIT, ptmi_api.cpp render; here forced on a small frame through 128-sample
+    chunks): the frame equals the uniform plan's up to FP64 summation order, with every
+    pixel's sample count exact, and equals the whole-tile render likewise."""
+    torch, sc = _torch_scene("teapot", 64, 48, 0.0, 0.0)
+    S, n = 600, 64 * 48
+    seeds = torch.tensor(layout.seeds_go_float64(n, 12), dtype=torch.float64, device="cuda")
+    frames = []
+    for ts in (1, 2, 3):
+        assert sc.set_knob(api.KNOB_MIN_CHUNK, 128) == api.PTMI_OK
+        assert sc.set_knob(api.KNOB_TAIL_SPLIT, ts) == api.PTMI_OK
+        f = torch.empty(n * 4, dtype=torch.float64, device="cuda")
+        sc.render(S, 0, S, seeds.data_ptr(), f.data_ptr())
+        frames.append(f)
+    whole = torch.empty(n * 4, dtype=torch.float64, device="cuda")
+    sc.render(S, 0, S, seeds.data_ptr(), whole.data_ptr(), chunks=1)
+    torch.cuda.synchronize()
+    sc.close()
+    for f in frames:
+        assert torch.all(f[3::4] == S)
+        assert (f - whole).abs().max().item() < 1e-12 * S
+    assert not torch.equal(frames[0], frames[1])  # the split plan sums other partials
+
+
 @pytest.mark.parametrize("scene,stride", [("reference", 1), ("reference", 3), ("teapot", 1), ("teapot", 2)])
 def test_whole_tiles_and_chunked_tail(scene, stride):
     """Automatic work plan (ptmi_device.h WorkPlan): whole-tile items first, the last
