@@ -56,7 +56,7 @@ for step in "$@"; do
       tail -12 $OUT/shards.log ;;
     shardsk)  # shardsk:<tag>:<cfgs>:<worlds>:<knobs, comma-separated NAME=VALUE>
       IFS=: read -r kind a b c d <<< "$step"
-      kn=""; for kv in ${d//,/ }; do kn="$kn --knob $kv"; done
+      kn=""; for kv in ${d//,/ }; do case $kv in split=*) kn="$kn --split ${kv#split=}";; *) kn="$kn --knob $kv";; esac; done
       timeout -k 10 600 python3 tools/shard_balance.py $OUT/shards_$a.json --configs $b --worlds $c $kn \
         > $OUT/shards_$a.log 2>&1 || { tail -20 $OUT/shards_$a.log; exit 1; }
       grep -E "^c[0-9] " $OUT/shards_$a.log ;;

@@ -30,6 +30,7 @@ ap.add_argument("out", nargs="?", default="")
 ap.add_argument("--configs", default="c2,c3,c4,c5")
 ap.add_argument("--worlds", default="2,4,8")
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--split", default="", help="sample|tile: override every config's split")
 ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
                 help="a work-plan knob of every scene (ptmi_diag_set_knob), as bench.py --knob")
 a = ap.parse_args()
@@ -38,6 +39,7 @@ XGMI_GBS = 153.0
 res = {"what": __doc__.strip().splitlines()[0], "device": api.device_name(0), "knobs": a.knob, "configs": {}}
 for cfg in a.configs.split(","):
     scene_name, W, H, S, aper, focal, split, _, desc = bench.CONFIGS[cfg]
+    split = a.split or split
     objs, tris, grps, cam = scene_inputs(scene_name, W, H, aper, focal)
     scene = api.Scene(0, objs, tris, grps, cam)
     for k, v in knobs:
