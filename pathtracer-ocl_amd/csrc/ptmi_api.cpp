@@ -33,7 +33,8 @@
 
 namespace ptmi {
 hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const double* seeds,
-                        const double* sunf, double* sums, double* part, hipStream_t st);
+                        const double* sunf, double* sums, double* part, uint32_t* item_ctr,
+                        hipStream_t st);
 hipError_t launch_sunflower(double* out, uint32_t samples, hipStream_t st);
 hipError_t launch_reduce(const double* part, double* sums, const WorkPlan& WP, int W, int H, bool planes,
                          hipStream_t st);
@@ -103,6 +104,7 @@ struct ptmi_scene {
     // of the last (tile_stride, tile_offset) rendered with one (see owned_tile).
     std::vector<uint32_t> tlist_host;
     uint32_t* tlist_dev = nullptr;
+    uint32_t* item_ctr = nullptr;  // the mesh kernels' work-item counter (ptmi_kernels.hip take_item), zeroed per launch
     uint32_t tlist_stride = 0, tlist_offset = 0, tlist_cap = 0;
     bool order_tlist = false;  // the dispatch order was built for a list launch
     uint32_t width = 0, height = 0;
@@ -866,6 +868,7 @@ void ptmi_scene_destroy(ptmi_scene* s) {
 #endif
     if (s->order_dev) (void)hipFree(s->order_dev);
     if (s->tlist_dev) (void)hipFree(s->tlist_dev);
+    if (s->item_ctr) (void)hipFree(s->item_ctr);
     if (s->cost_dev) (void)hipFree(s->cost_dev);
     for (auto& e : s->events) {
         (void)hipEventDestroy(e.first);
@@ -1108,6 +1111,10 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         HIP_TRY(hipMalloc((void**)&s->partial, need));
         s->partial_bytes = need;
     }
+    if (!split) {  // the launch's work-item counter, zeroed outside the timed span
+        if (!s->item_ctr) HIP_TRY(hipMalloc((void**)&s->item_ctr, 256));
+        HIP_TRY(hipMemsetAsync(s->item_ctr, 0, sizeof(uint32_t), st));
+    }
     if (ev0) HIP_TRY(hipEventRecord(ev0, st));
 #if PTMI_STUDY
     if (split) {
@@ -1116,7 +1123,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     } else
 #endif
     {
-        HIP_TRY(launch_trace(s->dev, kflags, samples, wp, seeds_dev, s->sunf, sums_dev, s->partial, st));
+        HIP_TRY(launch_trace(s->dev, kflags, samples, wp, seeds_dev, s->sunf, sums_dev, s->partial, s->item_ctr, st));
     }
     if (ev1) {
         HIP_TRY(hipEventRecord(ev1, st));

@@ -222,8 +222,17 @@ __device__ __forceinline__ d4 normv(d4 v) {
 __device__ __forceinline__ double max3(double a, double b, double c) { return fmax(fmax(a, b), c); }
 __device__ __forceinline__ double min3(double a, double b, double c) { return fmin(fmin(a, b), c); }
 
+// Uniform scene records (planes, spheres, group objects, traversal roots) are read through
+// the constant address space: read-only for the kernel's lifetime, they stay scalar loads
+// whatever the kernel writes before them (the mesh kernels' work-item atomic, take_item).
+template <typename T>
+using CPtr = const __attribute__((address_space(4))) T*;
+template <typename T>
+__device__ __forceinline__ CPtr<T> cmem(const T* p) { return (CPtr<T>)p; }
+
 // mul (tracer.cl:369-376): row-major mat4 x vec4, rows summed x+y+z+w.
-__device__ __forceinline__ d4 mat_mul(const double* __restrict__ m, d4 v) {
+template <typename M>
+__device__ __forceinline__ d4 mat_mul(M m, d4 v) {
     return mk(((m[0] * v.x + m[1] * v.y) + m[2] * v.z) + m[3] * v.w,
               ((m[4] * v.x + m[5] * v.y) + m[6] * v.z) + m[7] * v.w,
               ((m[8] * v.x + m[9] * v.y) + m[10] * v.z) + m[11] * v.w,
@@ -236,23 +245,25 @@ __device__ __forceinline__ d4 mat_mul(const double* __restrict__ m, d4 v) {
 // m0 x + m3 w bit-for-bit for a finite ray, up to the sign of an exact-zero
 // result, which no branch or output of the path depends on (rays are finite
 // here: see PathState::dead).
-__device__ __forceinline__ d4 xform_st(const double* __restrict__ m, d4 v) {
+template <typename M>
+__device__ __forceinline__ d4 xform_st(M m, d4 v) {
     return mk(m[0] * v.x + m[3] * v.w, m[5] * v.y + m[7] * v.w, m[10] * v.z + m[11] * v.w, m[15] * v.w);
 }
-__device__ __forceinline__ d4 xform(const double* __restrict__ m, bool st, d4 v) {
+template <typename M>
+__device__ __forceinline__ d4 xform(M m, bool st, d4 v) {
     return st ? xform_st(m, v) : mat_mul(m, v);
 }
 // mul(m, point) / mul(m, direction): in the affine case m * 1 == m and
 // m * 0 == +-0 make the w column an exact add of m[3] / a no-op, and row 3 is dead.
-template <bool A>
-__device__ __forceinline__ d4 xpt(const double* __restrict__ m, bool st, d4 v) {
+template <bool A, typename M>
+__device__ __forceinline__ d4 xpt(M m, bool st, d4 v) {
     if constexpr (!A) return xform(m, st, v);
     if (st) return mk(m[0] * v.x + m[3], m[5] * v.y + m[7], m[10] * v.z + m[11], 1.0);
     return mk(((m[0] * v.x + m[1] * v.y) + m[2] * v.z) + m[3], ((m[4] * v.x + m[5] * v.y) + m[6] * v.z) + m[7],
               ((m[8] * v.x + m[9] * v.y) + m[10] * v.z) + m[11], 1.0);
 }
-template <bool A>
-__device__ __forceinline__ d4 xdir(const double* __restrict__ m, bool st, d4 v) {
+template <bool A, typename M>
+__device__ __forceinline__ d4 xdir(M m, bool st, d4 v) {
     if constexpr (!A) return xform(m, st, v);
     if (st) return mk(m[0] * v.x, m[5] * v.y, m[10] * v.z, 0.0);
     return mk((m[0] * v.x + m[1] * v.y) + m[2] * v.z, (m[4] * v.x + m[5] * v.y) + m[6] * v.z,
@@ -753,7 +764,8 @@ struct WalkRay {
     float ohi[3];  // of * r - dt
     bool neg[3];   // r < 0
 };
-__device__ __forceinline__ WalkRay walk_setup(d4 o, d4 rw, const RootRec& R) {
+template <typename RR>  // RootRec, generic or constant address space
+__device__ __forceinline__ WalkRay walk_setup(d4 o, d4 rw, const RR& R) {
     const double oo[3] = {o.x, o.y, o.z}, rr[3] = {rw.x, rw.y, rw.z};
     float omax = 0.0f;
     float r[3], ofr[3];
@@ -899,8 +911,8 @@ __device__ __forceinline__ void leaf_visit(const DevScene& S, int first, int slo
 // child first, the others pushed far-to-near.  Which triangles are FOUND does
 // not depend on the visiting order or the widened boxes (every triangle that
 // can produce a winning t is reached); ties resolve through better_tri.
-template <bool kVerify, typename Stk>
-__device__ __forceinline__ void walk_index(const DevScene& S, Stk* __restrict__ stk, const RootRec& R, int slot,
+template <bool kVerify, typename Stk, typename RR>
+__device__ __forceinline__ void walk_index(const DevScene& S, Stk* __restrict__ stk, const RR& R, int slot,
                                            int key, d4 o, d4 d, d4 rw, Hit& h, int& vchain) {
     const int lb = leaf_bit_of<Stk>(S);
     const WalkRay W = walk_setup(o, rw, R);  // FP32 slab tests
@@ -951,8 +963,8 @@ __device__ __forceinline__ void walk_index(const DevScene& S, Stk* __restrict__ 
 // once per child walked into; leaves are visited in the stack walk's order, so the candidates
 // and hence the winner are the same (the pruning limit only shrinks: a child culled on a
 // re-test lies beyond the best hit, and so do its later siblings).
-template <bool kVerify>
-__device__ __forceinline__ void walk_index_stackless(const DevScene& S, const RootRec& R, int slot, int key, d4 o,
+template <bool kVerify, typename RR>
+__device__ __forceinline__ void walk_index_stackless(const DevScene& S, const RR& R, int slot, int key, d4 o,
                                                      d4 d, d4 rw, Hit& h, int& vchain) {
     const WalkRay W = walk_setup(o, rw, R);
     float lim = walk_limit(h.t);
@@ -1069,8 +1081,8 @@ __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int ke
 // reference's order, give oy and dy bit for bit up to the sign of an exact zero, which
 // neither t = -oy / dy nor its tests observe (t is then +-0, or |dy| is below EPSILON).
 // The walls of the reference scenes have one or two such zeros.
-template <int NZ>
-__device__ __forceinline__ void plane_rows_nz(const double* __restrict__ m, d4 ro, d4 rd, double& oy, double& dy) {
+template <int NZ, typename M>
+__device__ __forceinline__ void plane_rows_nz(M m, d4 ro, d4 rd, double& oy, double& dy) {
     static_assert(NZ >= 1 && NZ <= 7, "at least one live term");
     double o = 0.0, d = 0.0;
     bool any = false;
@@ -1101,8 +1113,8 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     // intersectPlane (478-483): row 1 only.  Planes are taken two at a time so the
     // two independent division chains overlap (then one odd plane).
     // Row 1 of mul() for the plane's origin and direction (intersectPlane, 478-483).
-    auto plane_rows = [&](const PlaneRec& P, double& oy, double& dy) {
-        const double* m = P.row1;
+    auto plane_rows = [&](const auto& P, double& oy, double& dy) {
+        const auto* m = P.row1;
         oy = ((m[0] * ro.x + m[1] * ro.y) + m[2] * ro.z) + (A ? m[3] : m[3] * ro.w);
         const double dy0 = (m[0] * rd.x + m[1] * rd.y) + m[2] * rd.z;
         dy = A ? dy0 : dy0 + m[3] * rd.w;
@@ -1125,12 +1137,12 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         k0 = big & (q0 > kEps);
         k1 = big & (q1 > kEps);
     };
-    auto plane_t = [&](const PlaneRec& P, double& q, bool& ok) {
+    auto plane_t = [&](const auto& P, double& q, bool& ok) {
         double oy, dy;
         plane_rows(P, oy, dy);
         plane_q(oy, dy, q, ok);
     };
-    auto plane_take = [&](const PlaneRec& P, double q, bool ok) {
+    auto plane_take = [&](const auto& P, double q, bool ok) {
         const bool c = ok & (q < h.t);
         h.t = c ? q : h.t;
         h.pk = c ? pack_hit(P.slot, P.key) : h.pk;
@@ -1143,7 +1155,7 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     if constexpr (A) {
         const int npy = (PTMI_ABLATE & 512) ? 0 : S.n_planes_y;  // DIAGNOSTIC 512: full rows for all
         for (; p + 1 < npy; p += 2) {
-            const PlaneRec P0 = S.planes[p], P1 = S.planes[p + 1];
+            const auto &P0 = cmem(S.planes)[p], &P1 = cmem(S.planes)[p + 1];
             double oy0, dy0, oy1, dy1, q0, q1;
             bool k0, k1;
             if (P0.par) {  // parallel pair: one product m1 y, one direction term, one reciprocal
@@ -1163,11 +1175,11 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         }
     }
     for (; p + 1 < np; p += 2) {
-        const PlaneRec P0 = S.planes[p], P1 = S.planes[p + 1];
+        const auto &P0 = cmem(S.planes)[p], &P1 = cmem(S.planes)[p + 1];
         double oy0, dy0, oy1, dy1, q0, q1;
         bool k0, k1;
         if (A && P0.par) {  // parallel pair: one sum of the origin's x, y, z terms, one direction term
-            const double* m = P0.row1;  // and one reciprocal (row1[0..2] of P1 are the same bits)
+            const auto* m = P0.row1;  // and one reciprocal (row1[0..2] of P1 are the same bits)
             const double a = (m[0] * ro.x + m[1] * ro.y) + m[2] * ro.z;
             oy0 = a + m[3];
             oy1 = a + P1.row1[3];
@@ -1183,14 +1195,14 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         plane_take(P1, q1, k1);
     }
     if (p < np) {
-        const PlaneRec P0 = S.planes[p];
+        const auto& P0 = cmem(S.planes)[p];
         double q0;
         bool k0;
         plane_t(P0, q0, k0);
         plane_take(P0, q0, k0);
     }
     const int nq = (PTMI_ABLATE & 16) ? 0 : S.n_spheres_st;
-    auto sphere_ray = [&](const SphereRec& Q, d4& o, d4& d) {
+    auto sphere_ray = [&](const auto& Q, d4& o, d4& d) {
         if constexpr (A) {
             o = mk(Q.m0 * ro.x + Q.m3, Q.m5 * ro.y + Q.m7, Q.m10 * ro.z + Q.m11, 1.0);
             d = mk(Q.m0 * rd.x, Q.m5 * rd.y, Q.m10 * rd.z, 0.0);
@@ -1221,7 +1233,7 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     };
     int q = 0;
     for (; q + 1 < nq; q += 2) {  // two spheres at a time: overlapping quadratic setups
-        const SphereRec Q0 = S.spheres[q], Q1 = S.spheres[q + 1];
+        const auto &Q0 = cmem(S.spheres)[q], &Q1 = cmem(S.spheres)[q + 1];
         d4 o0, d0, o1, d1;
         sphere_ray(Q0, o0, d0);
         sphere_ray(Q1, o1, d1);
@@ -1232,7 +1244,7 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         defer(a1, b1, disc1, Q1.slot, Q1.key);
     }
     if (q < nq) {
-        const SphereRec Q0 = S.spheres[q];
+        const auto& Q0 = cmem(S.spheres)[q];
         d4 o0, d0;
         sphere_ray(Q0, o0, d0);
         double a0, b0, disc0;
@@ -1242,13 +1254,13 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     if (pend) sphere_roots<A>(h, pa, pb, pd, pslot, pkey);
     int j = S.run_end[0];
     for (; j < S.run_end[1]; j++) {  // spheres with other matrices
-        const DevObject& ob = S.objs[j];
+        const auto& ob = cmem(S.objs)[j];
         if (ob.st) continue;  // in S.spheres
         sphere_test<A>(h, xpt<A>(ob.inv, false, ro), xdir<A>(ob.inv, false, rd), j, ob.key);
     }
     if (FL & F_CYLCUBE) {
         for (; j < S.run_end[2]; j++) {  // cylinders: intersectCylinder (396-446), caps disabled
-            const DevObject& ob = S.objs[j];
+            const auto& ob = cmem(S.objs)[j];
             d4 o = xpt<A>(ob.inv, ob.st, ro);
             d4 d = xdir<A>(ob.inv, ob.st, rd);
             double a = d.x * d.x + d.z * d.z;
@@ -1270,7 +1282,7 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
             }
         }
         for (; j < S.run_end[3]; j++) {  // cubes: intersectCube (378-394)
-            const DevObject& ob = S.objs[j];
+            const auto& ob = cmem(S.objs)[j];
             d4 o = xpt<A>(ob.inv, ob.st, ro);
             d4 d = xdir<A>(ob.inv, ob.st, rd);
             double x0, x1, y0, y1, z0, z1;
@@ -1296,12 +1308,12 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
 template <bool A>
 __device__ __forceinline__ bool group_needs_walk(const DevScene& S, d4 ro, d4 rd, const Hit& h) {
     for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
-        const DevObject& ob = S.objs[j];
+        const auto& ob = cmem(S.objs)[j];
         const d4 o = xpt<A>(ob.inv, ob.st, ro);
         const d4 d = xdir<A>(ob.inv, ob.st, rd);
         const d4 r = mk(rcp_walk(d.x), rcp_walk(d.y), rcp_walk(d.z), 0.0);
         for (int ci = 0; ci < ob.child_count; ci++) {
-            const RootRec& R = S.root_rec[ob.child_base + ci];
+            const auto& R = cmem(S.root_rec)[ob.child_base + ci];
             double tn;
             if (!cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
                           R.hull_mx[2], h.t + prune_margin(h.t), tn))
@@ -1318,7 +1330,7 @@ template <bool A, bool kVerify, typename Stk>
 __device__ __forceinline__ void group_walks_impl(const DevScene& S, Stk* __restrict__ stk, d4 ro, d4 rd, Hit& h,
                                                  bool& cert) {
     for (int j = S.run_end[3]; j < S.run_end[4]; j++) {
-        const DevObject& ob = S.objs[j];
+        const auto& ob = cmem(S.objs)[j];
         const d4 o = xpt<A>(ob.inv, ob.st, ro);
         const d4 d = xdir<A>(ob.inv, ob.st, rd);
         const d4 r = mk(rcp_walk(d.x), rcp_walk(d.y), rcp_walk(d.z), 0.0);
@@ -1328,7 +1340,7 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, Stk* __restr
         // verify_chain), not here.
         int vchain = -1;
         for (int ci = 0; ci < ob.child_count; ci++) {
-            const RootRec& R = S.root_rec[ob.child_base + ci];
+            const auto& R = cmem(S.root_rec)[ob.child_base + ci];
             double tn;
             if (cull_box(o, r, R.hull_mn[0], R.hull_mn[1], R.hull_mn[2], R.hull_mx[0], R.hull_mx[1],
                          R.hull_mx[2], h.t + prune_margin(h.t), tn))
@@ -2049,7 +2061,7 @@ __device__ __forceinline__ const DevScene& scene_reload(const DevScene& S) {
 template <int FL>
 __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t samples, const WorkPlan& WP,
                                              const double* __restrict__ seeds, const double* __restrict__ sunf,
-                                             double* __restrict__ sums, double* __restrict__ part) {
+                                             double* __restrict__ sums, double* __restrict__ part, uint32_t item) {
     constexpr bool A = !(FL & F_PROJ);
     constexpr bool kDof = (FL & F_DOF) != 0;
     constexpr int kCamComp = (kDof || !A) ? (A ? 6 : 8) : 3;  // see trace_kernel
@@ -2076,7 +2088,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t sample
 #if PTMI_STATS
     if (lane < 32) ptmi_wstat[0][lane] = 0;
 #endif
-    const Item it = work_item<(FL & F_TLIST) != 0>(S, WP, blockIdx.x, lane);
+    const Item it = work_item<(FL & F_TLIST) != 0>(S, WP, item, lane);
     if (!it.ok) return;
     const int px = it.px, py = it.py;
     // fgi / fgi2 (tracer.cl:839-841): double division rounded to float.
@@ -2246,7 +2258,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t sample
 #endif
     // The work item is re-derived (a few integer operations) rather than kept live across
     // the loop: its fields would hold ~5 VGPRs through every walk phase.
-    store_sums<false>(work_item<(FL & F_TLIST) != 0>(S, WP, blockIdx.x, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
+    store_sums<false>(work_item<(FL & F_TLIST) != 0>(S, WP, item, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
 }
 
 // Per-item duration onto its tile's cost accumulator (WorkPlan::cost, tile_order_kernel;
@@ -2259,9 +2271,10 @@ __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t sample
 #ifndef PTMI_TILE_COST
 #define PTMI_TILE_COST PTMI_STUDY  // the study build measures; the product does not
 #endif
-__device__ __forceinline__ void item_cost_add(const DevScene& S, const WorkPlan& WP, unsigned long long t0) {
+__device__ __forceinline__ void item_cost_add(const DevScene& S, const WorkPlan& WP, uint32_t item,
+                                              unsigned long long t0) {
     if (WP.cost && threadIdx.x == 0) {
-        const Item it = work_item(S, WP, blockIdx.x, 0);
+        const Item it = work_item(S, WP, item, 0);
         if (it.ok) {
             const uint32_t tiles_x = ((uint32_t)S.cam.width + kTile - 1) / kTile;
             atomicAdd(&WP.cost[(uint32_t)(it.py / kTile) * tiles_x + (uint32_t)(it.px / kTile)], wall_clock64() - t0);
@@ -2273,27 +2286,52 @@ __device__ __forceinline__ void item_cost_add(const DevScene& S, const WorkPlan&
 // over the whole sample range (sums -> the frame) or a sample chunk of a tail tile
 // (sums -> its slot of the partial buffer).  A wave that finishes frees its slot (LDS
 // included) at once.  RGB sums, A = #samples.
+// Which item a mesh kernel's workgroup runs: PTMI_ITEM_QUEUE 1 -- the next one in dispatch
+// order from a per-launch counter (one atomic per workgroup, zeroed before the launch), so
+// items go to whichever XCD frees a slot first instead of workgroup b's fixed XCD (b mod 8),
+// whose static eighth of the items made the XCDs of an 8-rank C5 share end up to 8 ms apart
+// (profiles/r5/timeline).  The scene records the kernel reads after it come through the
+// constant address space (cmem), so the atomic does not make them look clobbered to the
+// compiler's uniform-load analysis (with plain global reads 18 of trace_kernel<5>'s scalar
+// loads became vector loads and the frames lost 5.5 %, profiles/r5/item_queue).  Every item
+// writes only its own sums: the frame does not depend on the assignment.  The kernels without
+// meshes keep blockIdx.x.
+#ifndef PTMI_ITEM_QUEUE
+#define PTMI_ITEM_QUEUE 1
+#endif
+__device__ __forceinline__ uint32_t take_item(uint32_t* __restrict__ ctr) {
+#if PTMI_ITEM_QUEUE
+    uint32_t v = 0;
+    if (threadIdx.x == 0) v = atomicAdd(ctr, 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);  // lane 0: every lane is active here
+#else
+    (void)ctr;
+    return blockIdx.x;
+#endif
+}
 template <int FL>
 __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
                                                   : (FL & F_MATERIALS) ? PTMI_WAVES_MATERIALS
                                                                        : PTMI_WAVES) void trace_kernel(DevScene S, uint32_t samples, WorkPlan WP,
                                                     const double* __restrict__ seeds, const double* __restrict__ sunf,
-                                                    double* __restrict__ sums, double* __restrict__ part) {
+                                                    double* __restrict__ sums, double* __restrict__ part,
+                                                    uint32_t* __restrict__ item_ctr) {
 #if PTMI_TIMELINE
     const unsigned long long tl0 = wall_clock64();
 #endif
     if constexpr ((FL & F_GROUPS) != 0) {
+        const uint32_t item = take_item(item_ctr);
 #if PTMI_TILE_COST
         const unsigned long long c0 = WP.cost ? wall_clock64() : 0ull;
 #endif
-        trace_groups<FL>(S, samples, WP, seeds, sunf, sums, part);
+        trace_groups<FL>(S, samples, WP, seeds, sunf, sums, part, item);
 #if PTMI_TILE_COST
-        item_cost_add(S, WP, c0);
+        item_cost_add(S, WP, item, c0);
 #endif
 #if PTMI_TIMELINE
-        if (threadIdx.x == 0 && blockIdx.x < ptmi_tl_max) {
-            ptmi_tl[2 * blockIdx.x] = tl0;
-            ptmi_tl[2 * blockIdx.x + 1] = wall_clock64();
+        if (threadIdx.x == 0 && item < ptmi_tl_max) {
+            ptmi_tl[2 * item] = tl0;
+            ptmi_tl[2 * item + 1] = wall_clock64();
         }
 #endif
     } else {
@@ -3092,7 +3130,7 @@ const void* trace_kernel_symbol(int flags) {
 }
 
 hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const WorkPlan& WP, const double* seeds,
-                        const double* sunf, double* sums, double* part, hipStream_t st) {
+                        const double* sunf, double* sums, double* part, uint32_t* item_ctr, hipStream_t st) {
     const uint32_t items = WP.n_whole + WP.n_tail * WP.nchunks;
     if (items == 0) return hipSuccess;
     flags = kernel_flags(flags);
@@ -3101,7 +3139,7 @@ hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const Wo
     switch (flags) {
 #define K(f)                                                                                          \
     case f:                                                                                           \
-        hipLaunchKernelGGL(trace_kernel<f>, grid, block, 0, st, S, samples, WP, seeds, sunf, sums, part); \
+        hipLaunchKernelGGL(trace_kernel<f>, grid, block, 0, st, S, samples, WP, seeds, sunf, sums, part, item_ctr); \
         break;
         K(0) K(1) K(2) K(3) K(4) K(5) K(6) K(7) K(8) K(9) K(10) K(11) K(12) K(13) K(14) K(15)
         K(F_ALL | F_PROJ) K(F_ALL | F_PROJ | F_TEX)
