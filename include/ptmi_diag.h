@@ -83,6 +83,15 @@ int ptmi_diag_force_flags(int flags);
  * hemi_table_kernel): 0 on a sound toolchain; -1 for a NULL scene. */
 int ptmi_diag_hemi_mismatch(const ptmi_scene* s);
 
+/* The trace_kernel instantiation the scene's renders launch (its F_* kernel flags, e.g. 0 for
+ * the reference scene, 5 for teapot / gopher, 271 for an affine mesh scene with wide child
+ * codes, 31 for a non-affine scene); -1 for a NULL scene. */
+int ptmi_diag_scene_flags(const ptmi_scene* s);
+
+/* Tile ownership a tile-split ptmi_scene_render with this stride uses: 1 diagonal (tile (x, y)
+ * to rank (x + y) mod stride), 0 raster (tile t to rank t mod stride); -1 for bad arguments. */
+int ptmi_diag_tile_ownership(const ptmi_scene* s, uint32_t tile_stride);
+
 #ifdef __cplusplus
 }
 #endif

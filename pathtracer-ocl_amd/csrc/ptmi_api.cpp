@@ -46,6 +46,7 @@ hipError_t launch_combine(const double* parts, uint32_t nparts, size_t npix, dou
                           hipStream_t st);
 const void* trace_kernel_symbol(int flags);
 bool tile_list_supported(int flags);
+int trace_kernel_flags(int flags);
 #if PTMI_STUDY
 hipError_t launch_tile_order(unsigned long long* cost, uint32_t n_whole, uint32_t n_tail, uint32_t stride,
                              uint32_t offset, uint32_t* order, hipStream_t st);
@@ -403,15 +404,17 @@ int prepare_scene(const void* objects, uint32_t n_obj, const void* triangles, ui
     for (const DevObject& o : hs.objs)
         if (o.type == 1) affine = affine && tame(o.inv);
     if (!affine) flags |= 16;                                           // F_PROJ
-    // Child codes past 16 bits (>= 2^15 Node4s or triangles): the generic instantiations,
-    // whose traversal stack holds 32-bit entries (ptmi_kernels.hip walk_index).
-    if (hs.leaf_bit != kLeafNarrow) flags |= 16;
+    // Child codes past 16 bits (>= 2^15 Node4s or triangles): a traversal stack of 32-bit
+    // entries -- the affine F_WIDE instantiation (ptmi_kernels.hip trace_groups), or the
+    // generic one for non-affine scenes (round 5 sent every such scene to the generic one).
+    const int wide = hs.leaf_bit != kLeafNarrow ? 256 : 0;              // F_WIDE
     // Textured plane/sphere/cube colours or plane normal maps: the one textured
     // instantiation (generic arithmetic + software sampler, tracer.cl:907-914, 1077-1092).
     for (const DevObject& o : hs.objs)
         if ((o.tex && (o.type == 0 || o.type == 1 || o.type == 3)) || (o.tex_nm && o.type == 0)) flags = 63;
-    if (g_force_flags.load() >= 0) flags = g_force_flags.load() & 63;  // ptmi_diag_force_flags (tests)
-    if (hs.leaf_bit != kLeafNarrow) flags |= 16;  // (never a 16-bit stack for 31-bit codes)
+    const int forced = g_force_flags.load();  // ptmi_diag_force_flags (tests): one load
+    if (forced >= 0) flags = forced & 63;
+    flags |= wide;  // (never a 16-bit stack for 31-bit codes: F_PROJ and F_TEX kernels have 32-bit ones)
     if (textures) {
         for (int k = 0; k < 3; k++) {
             const uint64_t texels = (uint64_t)textures->width[k] * textures->height[k] * textures->count[k];
@@ -885,6 +888,19 @@ int ptmi_scene_size(const ptmi_scene* s, uint32_t* w, uint32_t* h) {
     return PTMI_OK;
 }
 
+// Tile ownership of a tile-split render (ptmi_scene_render): diagonal for affine narrow-code
+// mesh scenes in parity mode whose tile rows divide by the stride (the F_TLIST instantiations),
+// raster striding otherwise.  Exported as ptmi_diag_tile_ownership, so callers that mask shards
+// use the library's own decision (ptmi/dist.py had restated it).
+static bool diagonal_tiles(const ptmi_scene* s, uint32_t tile_stride) {
+    const int kflags0 = s->flags | (s->rng == PTMI_RNG_XOSHIRO ? 64 : 0);
+    const uint32_t tiles_x = (s->width + kTile - 1) / kTile;
+#if PTMI_STUDY
+    if (s->split) return false;
+#endif
+    return tile_stride > 1 && tile_list_supported(kflags0) && tiles_x % tile_stride == 0;
+}
+
 int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, uint32_t sample_end,
                       uint32_t tile_stride, uint32_t tile_offset, const double* seeds_dev, double* sums_dev,
                       uint32_t chunks, void* hip_stream, char* err, size_t err_len) {
@@ -907,12 +923,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     // tile (x, y) belongs to rank (x + y) mod stride, each row holding tiles_x / stride of a
     // rank's tiles -- through the F_TLIST instantiations (WorkPlan::tiles), so the one-GPU
     // kernels are untouched (profiles/r5/tile_skew).  Every pixel's sums are the same either way.
-#if PTMI_STUDY
-    const bool study_split = s->split;
-#else
-    constexpr bool study_split = false;
-#endif
-    const bool tlist = tile_stride > 1 && tile_list_supported(kflags0) && tiles_x % tile_stride == 0 && !study_split;
+    const bool tlist = diagonal_tiles(s, tile_stride);
     const uint32_t per_row = tiles_x / tile_stride;
     auto owned_tile = [&](uint32_t k) -> uint32_t {
         if (!tlist) return tile_offset + k * tile_stride;
@@ -1143,7 +1154,8 @@ int ptmi_scene_set_rng(ptmi_scene* s, int mode, char* err, size_t err_len) {
         return PTMI_ERR_ARG;
     }
     if (mode == PTMI_RNG_XOSHIRO && (s->flags & (16 | 32))) {  // F_PROJ | F_TEX
-        set_err(err, err_len, "the statistical RNG mode exists for affine, untextured scenes only");
+        set_err(err, err_len, "the statistical RNG mode exists for affine, untextured scenes only (this scene is %s)",
+                (s->flags & 32) ? "textured" : "not affine");
         return PTMI_ERR_UNSUPPORTED;
     }
     s->rng = mode;
@@ -1609,3 +1621,12 @@ extern "C" int ptmi_diag_force_flags(int flags) {
 }
 
 extern "C" int ptmi_diag_hemi_mismatch(const ptmi_scene* s) { return s ? s->hemi_mismatch : -1; }
+
+extern "C" int ptmi_diag_scene_flags(const ptmi_scene* s) {
+    return s ? trace_kernel_flags(s->flags | (s->rng == PTMI_RNG_XOSHIRO ? 64 : 0)) : -1;
+}
+
+extern "C" int ptmi_diag_tile_ownership(const ptmi_scene* s, uint32_t tile_stride) {
+    if (!s || tile_stride == 0) return -1;
+    return diagonal_tiles(s, tile_stride) ? 1 : 0;
+}

@@ -480,8 +480,11 @@ enum : int {
     F_PROJ = 16,      // not affine (see dotv): the literal double4 arithmetic, generic path only
     F_TEX = 32,       // textured objects: with F_ALL | F_PROJ, the one textured instantiation
     F_TLIST = 128,    // tile-split launch with an owned-tile list (WorkPlan::tiles): affine mesh kernels only
-    F_XRNG = 64       // opt-in statistical mode (ptmi_scene_set_rng): xoshiro128** instead of noise3D,
+    F_XRNG = 64,      // opt-in statistical mode (ptmi_scene_set_rng): xoshiro128** instead of noise3D,
                       // affine instantiations only; never the parity path
+    F_WIDE = 256      // affine mesh scene whose child codes need 31 bits (>= 2^15 Node4s or triangles):
+                      // the affine kernel with a 32-bit LDS traversal stack (one F_ALL | F_WIDE
+                      // instantiation, +- F_XRNG; ADVICE r5: such scenes had been sent to F_PROJ)
 };
 
 // The camera ray's two anti-aliasing offsets of sample n (tracer.cl:869).
@@ -840,8 +843,10 @@ __device__ __forceinline__ void node_children(const DevScene& S, int cur, const 
         return (float)__builtin_bit_cast(_Float16, (uint16_t)((i & 1) ? (w >> 16) : (w & 0xffffu)));
     };
 #if PTMI_STACKLESS
-    // (stackless study: child[0]'s high half holds the node's parent, finalize_index_codes)
-    const int ch[4] = {(int)(q[3].x & 0xFFFFu), (int)q[3].y, (int)q[3].z, (int)q[3].w};
+    // (stackless study: child[0]'s high half holds the node's parent -- finalize_index_codes packs
+    // it for narrow-code scenes only, so wide codes keep all their bits)
+    const bool packed = S.leaf_bit == kLeafNarrow;
+    const int ch[4] = {(int)(packed ? (q[3].x & 0xFFFFu) : q[3].x), (int)q[3].y, (int)q[3].z, (int)q[3].w};
     if (parent) *parent = (int)(q[3].x >> 16);
 #else
     const int ch[4] = {(int)q[3].x, (int)q[3].y, (int)q[3].z, (int)q[3].w};
@@ -1347,7 +1352,7 @@ __device__ __forceinline__ void group_walks_impl(const DevScene& S, Stk* __restr
                 continue;
             PTMI_TSTAMP(t_w);
 #if PTMI_STACKLESS
-            if constexpr (A) walk_index_stackless<kVerify>(S, R, j, ob.key, o, d, r, h, vchain);
+            if constexpr (A && sizeof(Stk) == 2) walk_index_stackless<kVerify>(S, R, j, ob.key, o, d, r, h, vchain);
             else
 #endif
             walk_index<kVerify>(S, stk, R, j, ob.key, o, d, r, h, vchain);
@@ -2071,7 +2076,9 @@ __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t sample
     // per-pixel colour sums (the same additions in the same order) and a parked lane's
     // primitive best (t, pk), which change once per path or per park, wait in LDS too:
     // registers are what the walk phases need.
-    __shared__ StackEntry<A> stk_lds[kStack * kStkStride];
+    // 16-bit entries unless the scene's codes are wide (F_WIDE: 6 KB per wave, 13.3 KB in all, so
+    // LDS then holds 12 waves per CU instead of 16).
+    __shared__ StackEntry<A && !(FL & F_WIDE)> stk_lds[kStack * kStkStride];
     __shared__ double acc_lds[3 * kBlock];
     // accumColor of the lane's current path in LDS (bounce_shade kAccLds), as in the kernels
     // without meshes: it changes only on bounces that see emission, and in registers the
@@ -2464,6 +2471,20 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
 #endif
     }
 }
+
+// scene_reload builds its pointer from the kernel-argument segment: it needs DevScene to be
+// trace_kernel's FIRST parameter.  Explicit kernel arguments are laid out from offset 0 in
+// declaration order (the hidden arguments follow them, AMDGPU code object v5), so this check on
+// the parameter list is what keeps the reload pointing at S.
+template <typename F>
+struct first_param;
+template <typename R, typename P0, typename... Ps>
+struct first_param<R (*)(P0, Ps...)> {
+    using type = P0;
+};
+static_assert(std::is_same<first_param<decltype(&trace_kernel<0>)>::type, DevScene>::value &&
+                  std::is_same<first_param<decltype(&trace_kernel<F_ALL>)>::type, DevScene>::value,
+              "scene_reload: DevScene must be trace_kernel's first parameter (kernarg offset 0)");
 
 #if PTMI_STUDY
 // ==== STUDY build only (make study -> build/libptmi_study.so) ==========================
@@ -2899,7 +2920,7 @@ __global__ __launch_bounds__(kBlock, PTMI_WALK_WAVES) void walk_split_kernel(Dev
 }
 
 bool split_supported(int flags) {
-    return (flags & F_GROUPS) && !(flags & (F_PROJ | F_TEX | F_XRNG));
+    return (flags & F_GROUPS) && !(flags & (F_PROJ | F_TEX | F_XRNG | F_WIDE));
 }
 
 const void* trace_split_symbol(int flags) {
@@ -2935,7 +2956,7 @@ hipError_t launch_split_pass(const DevScene& S, int flags, uint32_t samples, con
 hipError_t launch_walk(const DevScene& S, int flags, int mode, const WalkReq* req, uint32_t n, WalkRes* res,
                        uint32_t* next, uint32_t grid, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    if ((flags & (F_PROJ | F_TEX)) || !(flags & F_GROUPS)) return hipErrorInvalidValue;  // affine mesh scenes
+    if ((flags & (F_PROJ | F_TEX | F_WIDE)) || !(flags & F_GROUPS)) return hipErrorInvalidValue;  // affine narrow-code mesh scenes
     if (mode == 0) {
         hipLaunchKernelGGL(walk_kernel<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, S, req, n, res);
     } else {
@@ -3107,13 +3128,16 @@ int trace_tiles_per_block(int flags) { return 1; }
 static int kernel_flags(int flags) {
     if (flags & F_TEX) return F_ALL | F_PROJ | F_TEX;
     if (flags & F_PROJ) return F_ALL | F_PROJ;
+    if (flags & F_WIDE) return F_ALL | F_WIDE | (flags & F_XRNG);
     if ((flags & F_TLIST) && (flags & F_GROUPS) && !(flags & F_XRNG)) return flags & (F_ALL | F_TLIST);
     return flags & (F_ALL | F_XRNG);
 }
 
+int trace_kernel_flags(int flags) { return kernel_flags(flags); }
+
 // Whether a launch with these scene flags can take an owned-tile list (ptmi_api.cpp render).
 bool tile_list_supported(int flags) {
-    return (flags & F_GROUPS) && !(flags & (F_PROJ | F_TEX | F_XRNG));
+    return (flags & F_GROUPS) && !(flags & (F_PROJ | F_TEX | F_XRNG | F_WIDE));
 }
 
 const void* trace_kernel_symbol(int flags) {
@@ -3124,6 +3148,7 @@ const void* trace_kernel_symbol(int flags) {
         K(F_ALL | F_PROJ) K(F_ALL | F_PROJ | F_TEX)
         K(64) K(65) K(66) K(67) K(68) K(69) K(70) K(71) K(72) K(73) K(74) K(75) K(76) K(77) K(78) K(79)
         K(129) K(131) K(133) K(135) K(137) K(139) K(141) K(143)
+        K(F_ALL | F_WIDE) K(F_ALL | F_WIDE | F_XRNG)
 #undef K
     }
     return nullptr;
@@ -3145,6 +3170,7 @@ hipError_t launch_trace(const DevScene& S, int flags, uint32_t samples, const Wo
         K(F_ALL | F_PROJ) K(F_ALL | F_PROJ | F_TEX)
         K(64) K(65) K(66) K(67) K(68) K(69) K(70) K(71) K(72) K(73) K(74) K(75) K(76) K(77) K(78) K(79)
         K(129) K(131) K(133) K(135) K(137) K(139) K(141) K(143)
+        K(F_ALL | F_WIDE) K(F_ALL | F_WIDE | F_XRNG)
 #undef K
     default:
         return hipErrorInvalidValue;

@@ -114,7 +114,8 @@ def load_library(path=None):
         lib.ptmi_index_stats.argtypes = [vp, u32, vp, u32, vp, u32, vp, ctypes.POINTER(ctypes.c_double), i32, cp, sz]
     for name, args in (("ptmi_diag_set_knob", [vp, i32, i32]), ("ptmi_diag_force_flags", [i32]),
                        ("ptmi_diag_hemi_mismatch", [vp]), ("ptmi_diag_set_split", [vp, i32]),
-                       ("ptmi_diag_split_passes", [vp])):
+                       ("ptmi_diag_split_passes", [vp]), ("ptmi_diag_scene_flags", [vp]),
+                       ("ptmi_diag_tile_ownership", [vp, u32])):
         if hasattr(lib, name):  # (diagnostic libraries of earlier rounds lack some)
             getattr(lib, name).restype = i32
             getattr(lib, name).argtypes = args
@@ -311,6 +312,18 @@ class Scene:
         """ptmi_diag_hemi_mismatch: hemisphere-table records where the generic operator
         sequences differ from the affine ones the table holds (0 expected)."""
         return self._lib.ptmi_diag_hemi_mismatch(self._h)
+
+    def kernel_flags(self):
+        """ptmi_diag_scene_flags: F_* flags of the trace_kernel instantiation this scene launches."""
+        return self._lib.ptmi_diag_scene_flags(self._h)
+
+    def tile_ownership(self, tile_stride):
+        """ptmi_diag_tile_ownership: 'diagonal' or 'raster', the tile ownership a tile-split render
+        with this stride uses (the library's own decision; ptmi/dist.py tile_owner_mask takes it)."""
+        r = self._lib.ptmi_diag_tile_ownership(self._h, int(tile_stride))
+        if r < 0:
+            raise PtmiError(PTMI_ERR_ARG, "tile_ownership: bad stride %r" % (tile_stride,))
+        return "diagonal" if r == 1 else "raster"
 
     def set_timing(self, enable=True):
         self._lib.ptmi_scene_set_timing(self._h, 1 if enable else 0)

@@ -67,10 +67,21 @@ def shard(rank, world, samples, split):
 
 
 def diagonal_ownership(width, tile_stride, mesh_affine):
-    """Whether libptmi splits tiles diagonally (ptmi_api.cpp ptmi_scene_render): affine mesh
-    scenes whose tile rows divide by the stride; raster striding otherwise."""
+    """The library's tile-ownership rule for the common case (ptmi_api.cpp diagonal_tiles):
+    affine mesh scenes whose tile rows divide by the stride split diagonally, others raster.
+    `mesh_affine` must be False -- raster -- in the cases the library also excludes: the
+    statistical RNG mode, meshes with wide (31-bit) child codes (F_WIDE), non-affine or
+    textured scenes, and the study library's split form.  For a resident scene the library's
+    own decision is Scene.tile_ownership(stride) (ptmi_diag_tile_ownership); use that where a
+    scene is at hand (tests/test_gpu_parity.py checks the two agree)."""
     tx = (width + TILE - 1) // TILE
     return bool(mesh_affine) and tile_stride > 1 and tx % tile_stride == 0
+
+
+def scene_ownership_mask(scene, tile_stride, tile_offset):
+    """tile_owner_mask with the ownership a resident scene's renders use (the library's decision)."""
+    diag = scene.tile_ownership(tile_stride) == "diagonal"
+    return tile_owner_mask(scene.width, scene.height, tile_stride, tile_offset, diagonal=diag)
 
 
 def tile_owner_mask(width, height, tile_stride, tile_offset, diagonal=False):

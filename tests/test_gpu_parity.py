@@ -276,8 +276,8 @@ def test_mesh_tile_split_ownership(scene, stride):
     sc.render(S, 0, S, seeds.data_ptr(), full.data_ptr(), chunks=3)
     acc = torch.zeros_like(full)
     part = torch.empty_like(full)
-    diag = pdist.diagonal_ownership(W, stride, True)
-    assert diag == (stride != 3)
+    diag = sc.tile_ownership(stride) == "diagonal"  # the library's decision (ptmi_diag_tile_ownership)
+    assert diag == (stride != 3) == pdist.diagonal_ownership(W, stride, True)
     for g in range(stride):
         sc.render(S, 0, S, seeds.data_ptr(), part.data_ptr(), tile_stride=stride, tile_offset=g, chunks=3)
         torch.cuda.synchronize()
@@ -331,14 +331,19 @@ def _assert_ref_defined(objs, t2, g2, cam, spp, seeds):
 
 def test_hip_matches_live_reference_wide_child_codes():
     """A mesh past 16-bit child codes (tests/adversarial.py "big", 34,848 triangles) takes
-    the wide codes and the generic instantiation's 32-bit traversal stack: still the
-    reference's image."""
+    the wide codes and the affine F_WIDE instantiation's 32-bit traversal stack (round 6; it
+    had been sent to the generic instantiation): still the reference's image, and the generic
+    instantiation's bit for bit."""
     if not pyoracle.ref_available():
         pytest.skip("oracle/_ref not built")
     from tests import adversarial
     w, h, spp = 64, 48, 2
     objs, tris, grps, cam = adversarial.scene_inputs("big", w, h)
     assert api.index_stats(objs, tris, grps, cam)["leaf_bit"] == 0x40000000
+    sc = api.Scene(0, objs, tris, grps, cam)
+    assert sc.kernel_flags() == 15 | 256  # F_ALL | F_WIDE: affine, 32-bit stack
+    assert sc.tile_ownership(8) == "raster"  # no F_TLIST instantiation for wide codes
+    sc.close()
     seeds = layout.seeds_go_float64(w * h, 404)
     t2, g2 = layout.pad_empty(tris, grps)
     _assert_ref_defined(objs, t2, g2, cam, spp, seeds)
@@ -346,6 +351,35 @@ def test_hip_matches_live_reference_wide_child_codes():
     out = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
     err = np.abs(out - ref).max()
     assert err < 1e-12, "big: L-inf %.3e vs live reference" % err
+    with api.force_flags(31):  # the generic instantiation (literal double4 arithmetic)
+        gen = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
+    assert np.array_equal(out, gen)
+
+
+def test_wide_code_scene_statistical_rng():
+    """The statistical RNG mode on a wide-code mesh scene (F_WIDE | F_XRNG): allowed since the
+    scene stays on the affine kernels, deterministic, and back to the parity image when switched off."""
+    import torch
+    from tests import adversarial
+    w, h, spp = 64, 48, 2
+    objs, tris, grps, cam = adversarial.scene_inputs("big", w, h)
+    sc = api.Scene(0, objs, tris, grps, cam)
+    seeds = torch.tensor(layout.seeds_go_float64(w * h, 404), dtype=torch.float64, device="cuda")
+    out = torch.empty(w * h * 4, dtype=torch.float64, device="cuda")
+
+    def frame():
+        sc.render(spp, 0, spp, seeds.data_ptr(), out.data_ptr())
+        torch.cuda.synchronize()
+        return out.clone()
+
+    par = frame()
+    sc.set_rng(api.RNG_XOSHIRO)
+    assert sc.kernel_flags() == 15 | 256 | 64
+    x1, x2 = frame(), frame()
+    assert torch.equal(x1, x2) and not torch.equal(x1, par)
+    sc.set_rng(api.RNG_NOISE3D)
+    assert torch.equal(frame(), par)
+    sc.close()
 
 
 def test_hip_matches_oracle_past_reference_ctx():
