@@ -40,11 +40,20 @@
 // shade / whole loop [17] exact chain verifications [18] cycles in walk loops
 // [19] wave-level walk loop iterations [27] / [28] (mesh kernels, timers build) lane-cycles
 // of lanes whose work item is finished / all lane-cycles of the loop.
-__device__ unsigned long long ptmi_stats[40];
+// Round 6 (kernels without meshes, wave-level executions of each block, for the dynamic
+// instruction budget tools/dyn_budget.py): [32] camera refills [33] deferred sphere roots
+// [34] in-place sphere roots (a lane's second sphere) [35] hemisphere sincos fallback
+// [36] hemisphere sqrt fallback [37] / [38] / [39] noise draws with a lane below 2^17 / in
+// [2^17, 2^19) / at or above 2^19 [40] noise draws (any path) [41] plane normal block
+// [42] other-normal block [43] emission block [44] shading past the miss test [45] prims
+// [46] active lanes summed over the iterations that run prims; [47] / [48] / [49] floor-ceiling plane
+// pairs / other plane pairs / single planes [50] / [51] / [52] first sphere pair / later pairs / single
+// [53] iterations of the loop over spheres with other matrices.
+__device__ unsigned long long ptmi_stats[80];
 // Per-wave accumulators (one writer per wave: the first active lane), flushed to
 // ptmi_stats with one atomic per counter when the wave leaves its loop, so clock
 // and per-wave counts do not serialise on global atomics.
-__shared__ unsigned long long ptmi_wstat[1][32];
+__shared__ unsigned long long ptmi_wstat[1][64];
 #define PTMI_FIRST_ACTIVE() ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1)
 #define PTMI_WADD(i, v)                                                \
     do {                                                               \
@@ -88,6 +97,28 @@ __shared__ unsigned long long ptmi_wstat[1][32];
 // out of the product library.
 #ifndef PTMI_STUDY
 #define PTMI_STUDY 0
+#endif
+
+// Round-6 instruction cuts of the bounce loop (each a switch, measured one by one on the GPU;
+// profiles/r6/SUMMARY.md).  Every one leaves the images bit-identical.
+#ifndef PTMI_R6_LOOP
+#define PTMI_R6_LOOP 1  // the hit scoped to the active block (no loop-carried copies)
+#endif
+#ifndef PTMI_R6_SPH
+#define PTMI_R6_SPH 1  // deferred sphere roots: first sphere taken without selects, (slot, key) packed
+#endif
+#ifndef PTMI_R6_SLOT
+#define PTMI_R6_SLOT 1  // hemisphere-table slot test: one conversion pair, no range test
+#endif
+#ifndef PTMI_R6_FRACT
+#define PTMI_R6_FRACT 0  // noise fract as v_fract_f32 (exhaustively checked equal to ocml's fract)
+#endif
+#ifndef PTMI_R6_NPAIR
+#define PTMI_R6_NPAIR 0  // the two draws of a noise3D pair evaluated together (ptmi_sinf.h noise_sinf2):
+                         // 1 both sites, 2 camera only, 3 hemisphere only.  Measured C2 +0.6 % with 1
+#endif
+#ifndef PTMI_R6_SHLD
+#define PTMI_R6_SHLD 0  // shading: the hit object's record loads issued together, one wait
 #endif
 
 namespace ptmi {
@@ -301,9 +332,41 @@ __device__ __forceinline__ float noise3d(float x, float y, float z) {
     // ocml's sin_f32, bit for bit (ptmi_sinf.h noise_sinf): below 2^19 (every bench
     // argument) the specialised reduction, up to 2^30 (glass noise) an FP64 Cody-Waite
     // step, else and near ties ocml itself (out of line).
+#if PTMI_STATS
+    PTMI_WADD(40, 1ull);
+    if (__ballot(fabsf(s) < 0x1p17f)) PTMI_WADD(37, 1ull);
+    if (__ballot(fabsf(s) >= 0x1p17f && fabsf(s) < 0x1p19f)) PTMI_WADD(38, 1ull);
+    if (__ballot(!(fabsf(s) < 0x1p19f))) PTMI_WADD(39, 1ull);
+#endif
     const float sn = noise_sinf(s, [](float v) { return sinf_ocml(v); });
     float v = sn * 43758.5453f;
     return fminf(v - floorf(v), 0x1.fffffep-1f);
+}
+
+// Two noise3D draws at once (the camera's offsets, the hemisphere's uniforms): each draw's
+// arithmetic as in noise3d, the two sins through noise_sinf2, so the two dependent chains
+// interleave (round 6).  Bit-identical to two noise3d calls (tests/test_gpu_rng.py).
+__device__ __forceinline__ void noise3d_pair(float x1, float y1, float z1, float x2, float y2, float z2, float& u1,
+                                             float& u2) {
+    if (PTMI_ABLATE & 33) {  // (DIAGNOSTIC ablations of noise3d)
+        u1 = noise3d(x1, y1, z1);
+        u2 = noise3d(x2, y2, z2);
+        return;
+    }
+    const float s1 = (x1 * 112.9898f + y1 * 179.233f) + z1 * 237.212f;
+    const float s2 = (x2 * 112.9898f + y2 * 179.233f) + z2 * 237.212f;
+#if PTMI_STATS
+    PTMI_WADD(40, 2ull);
+    if (__ballot(fabsf(s1) < 0x1p17f || fabsf(s2) < 0x1p17f)) PTMI_WADD(37, 2ull);
+    if (__ballot((fabsf(s1) >= 0x1p17f && fabsf(s1) < 0x1p19f) || (fabsf(s2) >= 0x1p17f && fabsf(s2) < 0x1p19f)))
+        PTMI_WADD(38, 2ull);
+    if (__ballot(!(fabsf(s1) < 0x1p19f) || !(fabsf(s2) < 0x1p19f))) PTMI_WADD(39, 2ull);
+#endif
+    float sn1, sn2;
+    noise_sinf2(s1, s2, [](float v) { return sinf_ocml(v); }, sn1, sn2);
+    const float v1 = sn1 * 43758.5453f, v2 = sn2 * 43758.5453f;
+    u1 = fminf(v1 - floorf(v1), 0x1.fffffep-1f);
+    u2 = fminf(v2 - floorf(v2), 0x1.fffffep-1f);
 }
 
 // ---- Opt-in statistical RNG (F_XRNG, ptmi_scene_set_rng) ---------------------------
@@ -494,8 +557,12 @@ __device__ __forceinline__ void camera_offsets(float fgi, float fgi2, XSeed seed
     if constexpr ((FL & F_XRNG) != 0) {
         xcamera(seed_bits, n, rx, ry);
     } else {
-        rx = noise3d(fgi, (float)n, fgi2);
-        ry = noise3d(fgi, fgi2, (float)n);
+        if (PTMI_R6_NPAIR == 1 || PTMI_R6_NPAIR == 2) {
+            noise3d_pair(fgi, (float)n, fgi2, fgi, fgi2, (float)n, rx, ry);
+        } else {
+            rx = noise3d(fgi, (float)n, fgi2);
+            ry = noise3d(fgi, fgi2, (float)n);
+        }
     }
 }
 
@@ -1016,12 +1083,14 @@ __device__ __forceinline__ void walk_index_stackless(const DevScene& S, const RR
 
 // Candidate update as selects (no exec-mask branching).  t > EPSILON implies
 // the reference's `t != 0.0` recording test.
-__device__ __forceinline__ void consider_sel(Hit& h, double t, int obj, int key) {
-    const int pk = pack_hit(obj, key);
+__device__ __forceinline__ void consider_pk(Hit& h, double t, int pk) {
     const bool c = better(h, t, pk);
     h.t = c ? t : h.t;
     h.pk = c ? pk : h.pk;
     h.tri = c ? -1 : h.tri;
+}
+__device__ __forceinline__ void consider_sel(Hit& h, double t, int obj, int key) {
+    consider_pk(h, t, pack_hit(obj, key));
 }
 
 // intersectSphere (tracer.cl:448-476) on an object-space ray: the quadratic ...
@@ -1041,7 +1110,7 @@ __device__ __forceinline__ void sphere_quad(d4 o, d4 d, double& a, double& b, do
 // branch are the same.  disc > 0 is a difference of two doubles, so it is either
 // >= 2^-767 or so small that b is too (then both roots are below EPSILON).
 template <bool A>
-__device__ __forceinline__ void sphere_roots(Hit& h, double a, double b, double disc, int slot, int key) {
+__device__ __forceinline__ void sphere_roots(Hit& h, double a, double b, double disc, int pk) {
     if (A && !(PTMI_ABLATE & 128)) {
         // Both roots from one reciprocal of 2a (div_core_r: bit-identical to two div_core
         // calls), then one candidate: t1 if it is one, else t2 -- the reference records
@@ -1052,7 +1121,7 @@ __device__ __forceinline__ void sphere_roots(Hit& h, double a, double b, double 
             const double r = rcp_core(y);
             const double t1 = div_core_r(-b - sq, y, r);
             const double t2 = div_core_r(-b + sq, y, r);
-            consider_sel(h, t1 > kEps ? t1 : t2, slot, key);
+            consider_pk(h, t1 > kEps ? t1 : t2, pk);
         }
         return;
     }
@@ -1064,12 +1133,12 @@ __device__ __forceinline__ void sphere_roots(Hit& h, double a, double b, double 
         double t1 = (PTMI_ABLATE & 128) ? (-b - sq) * __builtin_amdgcn_rcp(2 * a)
                     : A                 ? div_core(-b - sq, 2 * a)
                                         : (-b - sq) / (2 * a);
-        consider_sel(h, t1, slot, key);
+        consider_pk(h, t1, pk);
         if (!(t1 > kEps)) {
             double t2 = (PTMI_ABLATE & 128) ? (-b + sq) * __builtin_amdgcn_rcp(2 * a)
                         : A                 ? div_core(-b + sq, 2 * a)
                                             : (-b + sq) / (2 * a);
-            consider_sel(h, t2, slot, key);
+            consider_pk(h, t2, pk);
         }
     }
 }
@@ -1077,7 +1146,7 @@ template <bool A>
 __device__ __forceinline__ void sphere_test(Hit& h, d4 o, d4 d, int slot, int key) {
     double a, b, disc;
     sphere_quad<A>(o, d, a, b, disc);
-    sphere_roots<A>(h, a, b, disc, slot, key);
+    sphere_roots<A>(h, a, b, disc, pack_hit(slot, key));
 }
 
 // Row 1 of mul() for a plane's origin and direction (intersectPlane, tracer.cl:478-483),
@@ -1160,6 +1229,7 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     if constexpr (A) {
         const int npy = (PTMI_ABLATE & 512) ? 0 : S.n_planes_y;  // DIAGNOSTIC 512: full rows for all
         for (; p + 1 < npy; p += 2) {
+            PTMI_WADD(47, 1ull);
             const auto &P0 = cmem(S.planes)[p], &P1 = cmem(S.planes)[p + 1];
             double oy0, dy0, oy1, dy1, q0, q1;
             bool k0, k1;
@@ -1180,6 +1250,7 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         }
     }
     for (; p + 1 < np; p += 2) {
+        PTMI_WADD(48, 1ull);
         const auto &P0 = cmem(S.planes)[p], &P1 = cmem(S.planes)[p + 1];
         double oy0, dy0, oy1, dy1, q0, q1;
         bool k0, k1;
@@ -1200,6 +1271,7 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         plane_take(P1, q1, k1);
     }
     if (p < np) {
+        PTMI_WADD(49, 1ull);
         const auto& P0 = cmem(S.planes)[p];
         double q0;
         bool k0;
@@ -1224,20 +1296,47 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
     // (better()), so the order of evaluation does not matter.
     bool pend = false;
     double pa = 0.0, pb = 0.0, pd = 0.0;
-    int pslot = 0, pkey = 0;
+    int ppk = 0;
     auto defer = [&](double a, double b, double disc, int slot, int key) {
         const bool has = disc > 0.0;
-        if (has && pend) sphere_roots<A>(h, a, b, disc, slot, key);
+        const int pk = pack_hit(slot, key);  // (uniform: scalar)
+        if (has && pend) {
+            PTMI_WADD(34, 1ull);
+            sphere_roots<A>(h, a, b, disc, pk);
+        }
         const bool take = has && !pend;
         pa = take ? a : pa;
         pb = take ? b : pb;
         pd = take ? disc : pd;
-        pslot = take ? slot : pslot;
-        pkey = take ? key : pkey;
+        ppk = take ? pk : ppk;
         pend = pend || has;
     };
+    // The first sphere's quadratic is kept as it is (round 6): nothing is pending before it, so
+    // its selects would only choose between it and the initial zeros, which are never read
+    // unless pend is set.
+    auto first = [&](double a, double b, double disc, int slot, int key) {
+        pa = a;
+        pb = b;
+        pd = disc;
+        ppk = pack_hit(slot, key);
+        pend = disc > 0.0;
+    };
     int q = 0;
+    if (PTMI_R6_SPH && nq >= 2) {
+        PTMI_WADD(50, 1ull);
+        const auto &Q0 = cmem(S.spheres)[0], &Q1 = cmem(S.spheres)[1];
+        d4 o0, d0, o1, d1;
+        sphere_ray(Q0, o0, d0);
+        sphere_ray(Q1, o1, d1);
+        double a0, b0, disc0, a1, b1, disc1;
+        sphere_quad<A>(o0, d0, a0, b0, disc0);
+        sphere_quad<A>(o1, d1, a1, b1, disc1);
+        first(a0, b0, disc0, Q0.slot, Q0.key);
+        defer(a1, b1, disc1, Q1.slot, Q1.key);
+        q = 2;
+    }
     for (; q + 1 < nq; q += 2) {  // two spheres at a time: overlapping quadratic setups
+        PTMI_WADD(51, 1ull);
         const auto &Q0 = cmem(S.spheres)[q], &Q1 = cmem(S.spheres)[q + 1];
         d4 o0, d0, o1, d1;
         sphere_ray(Q0, o0, d0);
@@ -1249,16 +1348,25 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         defer(a1, b1, disc1, Q1.slot, Q1.key);
     }
     if (q < nq) {
+        PTMI_WADD(52, 1ull);
         const auto& Q0 = cmem(S.spheres)[q];
         d4 o0, d0;
         sphere_ray(Q0, o0, d0);
         double a0, b0, disc0;
         sphere_quad<A>(o0, d0, a0, b0, disc0);
-        defer(a0, b0, disc0, Q0.slot, Q0.key);
+        if (PTMI_R6_SPH && q == 0) first(a0, b0, disc0, Q0.slot, Q0.key);
+        else defer(a0, b0, disc0, Q0.slot, Q0.key);
     }
-    if (pend) sphere_roots<A>(h, pa, pb, pd, pslot, pkey);
+    if (pend) {
+        PTMI_WADD(33, 1ull);
+        sphere_roots<A>(h, pa, pb, pd, ppk);
+    }
     int j = S.run_end[0];
-    for (; j < S.run_end[1]; j++) {  // spheres with other matrices
+    // spheres with other matrices (none when every sphere is in S.spheres: the loop's scalar
+    // record loads and waits are skipped)
+    if (PTMI_R6_SPH && S.run_end[1] - j == S.n_spheres_st) j = S.run_end[1];
+    for (; j < S.run_end[1]; j++) {
+        PTMI_WADD(53, 1ull);
         const auto& ob = cmem(S.objs)[j];
         if (ob.st) continue;  // in S.spheres
         sphere_test<A>(h, xpt<A>(ob.inv, false, ro), xdir<A>(ob.inv, false, rd), j, ob.key);
@@ -1465,6 +1573,9 @@ static constexpr int kHemiSize = 1 << kHemiBits;
 __device__ __forceinline__ int hemi_slot(float u) {  // table record of u, or -1 off the grid
     const float t = u * (float)kHemiSize;  // exact (power of two)
     const int k = (int)t;
+    // Every uniform is in [0, 1) (noise3d's fract is at most 0x1.fffffep-1, xnext16 < 1), so k is
+    // below kHemiSize whenever t is an integer; a NaN fails the equality.
+    if (PTMI_R6_SLOT) return t == (float)k ? k : -1;
     return (t == (float)k && (unsigned)k < (unsigned)kHemiSize) ? k : -1;
 }
 
@@ -1477,6 +1588,7 @@ __device__ __forceinline__ d4 random_hemisphere(const double* __restrict__ tab, 
         sr = q.x;
         cr = q.y;
     } else {
+        PTMI_WADD(35, 1ull);
         hemi_sincos<A>(u1, sr, cr);
     }
     const int k2 = kTab ? hemi_slot(u2) : -1;
@@ -1485,6 +1597,7 @@ __device__ __forceinline__ d4 random_hemisphere(const double* __restrict__ tab, 
         rand2s = q.x;
         rc = q.y;
     } else {
+        PTMI_WADD(36, 1ull);
         hemi_sqrt<A>(u2, rand2s, rc);
     }
     // cross(axis, n) for a unit axis: the fma chains of opencl.bc's cross reduce
@@ -1763,6 +1876,7 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
     constexpr bool A = !(FL & F_PROJ);
     constexpr bool kX = (FL & F_XRNG) != 0;
     if (h.pk < 0) return true;  // a miss repeats identically until b == 10 in the reference
+    PTMI_WADD(44, 1ull);
     const DevObject& ob = S.objs[h.pk & 0xFFFF];
     const int type = ob.type;
     const uint32_t b = P.b;
@@ -1770,9 +1884,52 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
     d4 eye = mk(-P.rd.x, -P.rd.y, -P.rd.z, -P.rd.w);
     // Object normal -> world normal (tracer.cl:903-955).
     d4 nv;
-    if (type == 0 && !((FL & F_TEX) && ob.tex_nm)) {
+    // Kernels whose objects are planes and spheres only (no cylinders, cubes, meshes or textures):
+    // every record field either normal needs is loaded up front -- one wait for the lot instead
+    // of a chain of dependent loads behind the type, st and invt_diag branches -- and the
+    // scale+translate sphere normal is computed for every lane, then selected: a wave almost
+    // always holds both kinds of hit, so both were run anyway (round 6).  The arithmetic is the
+    // branchy path's (xpt with st, the diagonal inverse transpose, norm3_core); a sphere without
+    // those patterns takes the general code.
+    constexpr bool kFlat = PTMI_R6_SHLD && A && !(FL & (F_TEX | F_CYLCUBE | F_GROUPS));
+    if constexpr (kFlat) {
+        const double* R = ob.inv;
+        const double2 i0 = *reinterpret_cast<const double2*>(R + 0);    // inv[0], inv[1]
+        const double2 i2 = *reinterpret_cast<const double2*>(R + 2);    // inv[2], inv[3]
+        const double2 i4 = *reinterpret_cast<const double2*>(R + 4);    // inv[4], inv[5]
+        const double2 i6 = *reinterpret_cast<const double2*>(R + 6);    // inv[6], inv[7]
+        const double2 i10 = *reinterpret_cast<const double2*>(R + 10);  // inv[10], inv[11]
+        const double2 t0 = *reinterpret_cast<const double2*>(ob.inv_t + 0);
+        const double2 t4 = *reinterpret_cast<const double2*>(ob.inv_t + 4);
+        const double2 t10 = *reinterpret_cast<const double2*>(ob.inv_t + 10);
+        const double2 pn = *reinterpret_cast<const double2*>(ob.plane_n);
+        const double pnz = ob.plane_n[2];
+        const int2 pat = *reinterpret_cast<const int2*>(&ob.st);  // st, invt_diag
+        const bool sph = type == 1;
+        PTMI_WADD(41, 1ull);
+        // xpt (st): (m0 x + m3, m5 y + m7, m10 z + m11); on = lp - (0, 0, 0); invT diagonal
+        const d4 ns = norm3_core(mk(t0.x * (i0.x * pos.x + i2.y), t4.y * (i4.y * pos.y + i6.y),
+                                    t10.x * (i10.x * pos.z + i10.y), 0.0));
+        nv = sph ? ns : mk(pn.x, pn.y, pnz, 0.0);
+        if (sph && !(pat.x != 0 && pat.y != 0)) {
+            PTMI_WADD(42, 1ull);
+            const d4 lp = xpt<A>(ob.inv, ob.st, pos);
+            const d4 on = mk(lp.x - 0.0, lp.y - 0.0, lp.z - 0.0, 0.0);
+            const double* it = ob.inv_t;
+            d4 g;
+            if (ob.invt_diag) {
+                g = mk(it[0] * on.x, it[5] * on.y, it[10] * on.z, 0.0);
+            } else {
+                g = mk((it[0] * on.x + it[1] * on.y) + it[2] * on.z, (it[4] * on.x + it[5] * on.y) + it[6] * on.z,
+                       (it[8] * on.x + it[9] * on.y) + it[10] * on.z, 0.0);
+            }
+            nv = norm3_core(g);
+        }
+    } else if (type == 0 && !((FL & F_TEX) && ob.tex_nm)) {
+        PTMI_WADD(41, 1ull);
         nv = ld4(ob.plane_n);  // constant per plane: normalize(mul(invT, (0,1,0,0))), w = 0
     } else {
+        PTMI_WADD(42, 1ull);
         d4 on;
         if ((FL & F_TEX) && type == 0) {
             on = plane_normal_map<A>(S.tex[0], ob, pos);
@@ -1850,6 +2007,8 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
         if constexpr (kX) {
             u1 = xnext16(P.rng);
             u2 = xnext16(P.rng);
+        } else if (PTMI_R6_NPAIR == 1 || PTMI_R6_NPAIR == 3) {
+            noise3d_pair(fgi, (float)b, (float)n, (float)b, (float)n, fgi, u1, u2);
         } else {
             u1 = noise3d(fgi, (float)b, (float)n);
             u2 = noise3d((float)b, (float)n, fgi);
@@ -1902,6 +2061,7 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
             P.ab = P.ab + mb * eb;
         }
         if (er > 0.0) {
+            PTMI_WADD(43, 1ull);
             if (b == 0) {  // the reduction's first record (tracer.cl:1160): records are per bounce, so x == b
                 if constexpr (kAccLds) {
                     acm[0 * kBlock] = cr;
@@ -2093,7 +2253,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t sample
     __shared__ double cam_lds[kCamComp * kBlock];
     const int tid = threadIdx.x, lane = tid & 63;
 #if PTMI_STATS
-    if (lane < 32) ptmi_wstat[0][lane] = 0;
+    ptmi_wstat[0][lane] = 0;
 #endif
     const Item it = work_item<(FL & F_TLIST) != 0>(S, WP, item, lane);
     if (!it.ok) return;
@@ -2260,7 +2420,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t sample
     PTMI_TADD(16, t_loop);
 #if PTMI_STATS
     if (PTMI_FIRST_ACTIVE())
-        for (int k = 0; k < 32; k++)
+        for (int k = 0; k < 64; k++)
             if (ptmi_wstat[0][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[0][k]);
 #endif
     // The work item is re-derived (a few integer operations) rather than kept live across
@@ -2345,7 +2505,7 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
         constexpr bool A = !(FL & F_PROJ);
         const int tid = threadIdx.x, lane = tid & 63;
 #if PTMI_STATS
-        if (lane < 32) ptmi_wstat[0][lane] = 0;
+        ptmi_wstat[0][lane] = 0;
 #endif
         const Item it = work_item(S, WP, blockIdx.x, lane);
         if (!it.ok) return;
@@ -2394,6 +2554,7 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
             const int n_starve = __popcll(__ballot(!buffered && !active && n_gen < c_end));
             if (n_need >= kRefillNeed || n_starve >= PTMI_REFILL_STARVE || (n_starve > 0 && !__any(active))) {
                 const DevCamera& cam = camera_ptr<(PTMI_CAM_RELOAD & 1) != 0>(S);
+                PTMI_WADD(32, 1ull);
                 if (need) {
                     d4 ro, rd;
                     float rx, ry;
@@ -2438,6 +2599,28 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
                 active = true;
             }
             PTMI_TADD(12, t_a);
+#if PTMI_R6_LOOP
+            // The hit lives only inside the active block (round 6): declared outside it, the
+            // uninitialised Hit of inactive lanes became loop-carried registers, copied at every
+            // iteration (6 v_mov_b64 per bounce).
+            if (active) {
+                PTMI_TSTAMP(t_b);
+                PTMI_WADD(45, 1ull);
+                PTMI_WADD(46, (unsigned long long)__popcll(__ballot(1)));
+                Hit h;
+                if (P.dead) h.pk = -1;
+                else h = find_closest_prims<FL>(S, P.ro, P.rd);
+                PTMI_TADD(13, t_b);
+                PTMI_TSTAMP(t_d);
+                if (bounce_shade<FL, true>(S, P, h, fgi, n_cur, acm)) {
+                    acc[0 * kBlock] = acc[0 * kBlock] + acm[0 * kBlock];  // colors += accumColor (tracer.cl:1179)
+                    acc[1 * kBlock] = acc[1 * kBlock] + acm[1 * kBlock];
+                    acc[2 * kBlock] = acc[2 * kBlock] + acm[2 * kBlock];
+                    active = false;
+                }
+                PTMI_TADD(15, t_d);
+            }
+#else
             PTMI_TSTAMP(t_b);
             Hit h;
             if (active) {
@@ -2453,12 +2636,13 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
                 active = false;
             }
             PTMI_TADD(15, t_d);
+#endif
             PTMI_WADD(10, 1ull);
         }
         PTMI_TADD(16, t_loop);
 #if PTMI_STATS
         if (PTMI_FIRST_ACTIVE())
-            for (int k = 0; k < 32; k++)
+            for (int k = 0; k < 64; k++)
                 if (ptmi_wstat[0][k]) atomicAdd(&ptmi_stats[k], ptmi_wstat[0][k]);
 #endif
         store_sums<true>(work_item(S, WP, blockIdx.x, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock],
@@ -3253,9 +3437,9 @@ hipError_t launch_seeds(double* seeds, uint32_t n, uint64_t stream, hipStream_t 
 #if PTMI_STATS
 namespace ptmi {
 int stats_read(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi_stats), sizeof(unsigned long long) * 40) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ptmi_stats), sizeof(unsigned long long) * 80) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[40] = {0};
+        unsigned long long z[80] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(ptmi_stats), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

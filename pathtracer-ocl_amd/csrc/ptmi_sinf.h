@@ -145,6 +145,23 @@ PTMI_SINF_FN float sf_redux_large_17_19(float x, int& q) {
     return e1 + p;
 }
 
+// __ocmlpriv_sincosred_f32 on the reduced argument r (quadrant q) and the quadrant / sign
+// fix-ups of __ocml_sin_f32 for x (ax = |x|).
+PTMI_SINF_FN float sf_sin_poly(float x, float ax, float r, int q) {
+    const float x2 = r * r;
+    float s = fmaf(x2, sf_float(0xB94C1982u), sf_float(0x3C0881C4u));
+    s = fmaf(x2, s, sf_float(0xBE2AAA9Du));
+    s = x2 * s;
+    s = fmaf(r, s, r);
+    float c = fmaf(x2, sf_float(0x37D75334u), sf_float(0xBAB64F3Bu));
+    c = fmaf(x2, c, sf_float(0x3D2AABF7u));
+    c = fmaf(x2, c, sf_float(0xBF000004u));
+    c = fmaf(x2, c, 1.0f);
+    const uint32_t v = (q & 1) ? sf_bits(c) : sf_bits(s);
+    const uint32_t neg = (q > 1) ? 0x80000000u : 0u;
+    return sf_float((sf_bits(ax) ^ sf_bits(x)) ^ neg ^ v);
+}
+
 // __ocml_sin_f32 for finite |x| < 2^19 (callers route everything else to ocml).
 PTMI_SINF_FN float sinf_lt19(float x) {
     const float ax = fabsf(x);
@@ -219,6 +236,62 @@ PTMI_SINF_FN float noise_sinf(float x, Fallback fallback) {
         sn = fallback(x);
     }
     return sn;
+}
+
+// The FP64 Cody-Waite step of sf_redux_large_17_19 alone (2^17 <= ax < 2^19): true, with ocml's
+// r and q, on every argument but the ~28 per 2^24 that sf_redux_large_17_19 hands to its
+// Payne-Hanek product.
+PTMI_SINF_FN bool sf_cw64(float ax, float& rf, int& q) {
+    const double xd = (double)ax;
+    const double kd = __builtin_rint(xd * 0x1.45f306dc9c883p-1);
+    double r = fma(-kd, 0x1.921fb54400000p+0, xd);
+    r = fma(-kd, 0x1.0b4611a600000p-34, r);
+    r = fma(-kd, 0x1.3198a2e037073p-69, r);
+    const uint64_t rb = __builtin_bit_cast(uint64_t, r);
+    const uint32_t tail = ((uint32_t)rb + 0x200u) & 0x1FFFFFFFu;
+    q = ((int)kd) & 3;
+    rf = (float)r;
+    return ((uint32_t)(rb >> 32) & 0x7FFFFFFFu) < 0x3FE921FBu && tail - 0x10000000u >= 0x400u;
+}
+
+// Two noise sins at once (round 6): noise_sinf(x1) and noise_sinf(x2), bit for bit.  The two
+// draws of a noise3D pair (the camera's anti-aliasing offsets, the hemisphere's uniforms) are
+// independent; evaluated one after the other their branchy reductions run as separate blocks and
+// each dependent chain is exposed in turn.  Here each reduction block serves both draws (a block
+// runs when either draw needs it), so the two chains interleave.  Lanes with an argument the
+// common blocks do not finish -- the Payne-Hanek band of [2^17, 2^19) and |x| >= 2^19 -- take
+// noise_sinf itself afterwards.
+template <typename Fallback>
+PTMI_SINF_FN void noise_sinf2(float x1, float x2, Fallback fallback, float& o1, float& o2) {
+    const float a1 = fabsf(x1), a2 = fabsf(x2);
+    const bool sm1 = a1 < 131072.0f, sm2 = a2 < 131072.0f;
+    bool ok1 = a1 < 0x1p19f, ok2 = a2 < 0x1p19f;  // (NaN: false)
+    float r1 = 0.0f, r2 = 0.0f;
+    int q1 = 0, q2 = 0;
+    if (sm1 || sm2) {
+        int qa, qb;
+        const float ra = sf_redux_small(a1, qa), rb = sf_redux_small(a2, qb);
+        r1 = sm1 ? ra : r1;
+        q1 = sm1 ? qa : q1;
+        r2 = sm2 ? rb : r2;
+        q2 = sm2 ? qb : q2;
+    }
+    const bool lg1 = ok1 && !sm1, lg2 = ok2 && !sm2;
+    if (lg1 || lg2) {
+        float ra, rb;
+        int qa, qb;
+        const bool ca = sf_cw64(a1, ra, qa), cb = sf_cw64(a2, rb, qb);
+        r1 = lg1 ? ra : r1;
+        q1 = lg1 ? qa : q1;
+        r2 = lg2 ? rb : r2;
+        q2 = lg2 ? qb : q2;
+        ok1 = ok1 && (sm1 || ca);
+        ok2 = ok2 && (sm2 || cb);
+    }
+    o1 = sf_sin_poly(x1, a1, r1, q1);
+    o2 = sf_sin_poly(x2, a2, r2, q2);
+    if (!ok1) o1 = noise_sinf(x1, fallback);
+    if (!ok2) o2 = noise_sinf(x2, fallback);
 }
 
 }  // namespace ptmi

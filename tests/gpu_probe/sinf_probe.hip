@@ -226,3 +226,84 @@ extern "C" int probe_ptmi_noise_sinf_all(unsigned long long* mismatches, unsigne
     (void)hipFree(dfb);
     return 0;
 }
+
+// The paired noise sin (ptmi_sinf.h noise_sinf2, round 6) against noise_sinf for every float in
+// the first slot, paired with a second float drawn from the whole bit space (a bijective mix of the
+// first's bits, so every float is also checked in the second slot).
+__device__ static inline uint32_t pair_mix(uint32_t b) {
+    b ^= b >> 16;
+    b *= 0x7FEB352Du;
+    b ^= b >> 15;
+    b *= 0x846CA68Bu;
+    b ^= b >> 16;
+    return b;
+}
+__global__ void ptmi_noise_sinf2_check(uint64_t base, uint64_t count, unsigned long long* mism, unsigned int* first) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t bits = (uint32_t)(base + i);
+    const float x1 = pto_bits2f(bits), x2 = pto_bits2f(pair_mix(bits));
+    auto fb = [](float v) { return sinf(v); };
+    float o1, o2;
+    ptmi::noise_sinf2(x1, x2, fb, o1, o2);
+    const float e1 = ptmi::noise_sinf(x1, fb), e2 = ptmi::noise_sinf(x2, fb);
+    const bool ok1 = pto_f2bits(o1) == pto_f2bits(e1) || (o1 != o1 && e1 != e1);
+    const bool ok2 = pto_f2bits(o2) == pto_f2bits(e2) || (o2 != o2 && e2 != e2);
+    if (!(ok1 && ok2)) {
+        atomicAdd(mism, 1ull);
+        atomicMin(first, bits);
+    }
+}
+
+extern "C" int probe_ptmi_noise_sinf2_all(unsigned long long* mismatches, unsigned int* first_bad) {
+    unsigned long long* dm;
+    unsigned int* df;
+    if (hipMalloc(&dm, 8) || hipMalloc(&df, 4)) return -1;
+    (void)hipMemset(dm, 0, 8);
+    (void)hipMemset(df, 0xff, 4);
+    const uint64_t chunk = 1ull << 28;
+    for (uint64_t base = 0; base < (1ull << 32); base += chunk) {
+        hipLaunchKernelGGL(ptmi_noise_sinf2_check, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, chunk, dm, df);
+        if (hipGetLastError() != hipSuccess) return -2;
+    }
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    (void)hipMemcpy(mismatches, dm, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(first_bad, df, 4, hipMemcpyDeviceToHost);
+    (void)hipFree(dm);
+    (void)hipFree(df);
+    return 0;
+}
+
+// v_fract_f32 (__builtin_amdgcn_fractf) against ocml's fract, min(x - floor(x), 0x1.fffffep-1), for
+// every finite float: whether noise3d may use the one instruction (PTMI_R6_FRACT).
+__global__ void fract_check(uint64_t base, uint64_t count, unsigned long long* mism, unsigned int* first) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t bits = (uint32_t)(base + i);
+    const float x = pto_bits2f(bits);
+    if (!isfinite(x)) return;
+    const float a = __builtin_amdgcn_fractf(x), b = fminf(x - floorf(x), 0x1.fffffep-1f);
+    if (pto_f2bits(a) != pto_f2bits(b)) {
+        atomicAdd(mism, 1ull);
+        atomicMin(first, bits);
+    }
+}
+
+extern "C" int probe_fract_all(unsigned long long* mismatches, unsigned int* first_bad) {
+    unsigned long long* dm;
+    unsigned int* df;
+    if (hipMalloc(&dm, 8) || hipMalloc(&df, 4)) return -1;
+    (void)hipMemset(dm, 0, 8);
+    (void)hipMemset(df, 0xff, 4);
+    const uint64_t chunk = 1ull << 28;
+    for (uint64_t base = 0; base < (1ull << 32); base += chunk) {
+        hipLaunchKernelGGL(fract_check, dim3((unsigned)(chunk / 256)), dim3(256), 0, 0, base, chunk, dm, df);
+        if (hipGetLastError() != hipSuccess) return -2;
+    }
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    (void)hipMemcpy(mismatches, dm, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(first_bad, df, 4, hipMemcpyDeviceToHost);
+    (void)hipFree(dm);
+    (void)hipFree(df);
+    return 0;
+}

@@ -23,6 +23,8 @@ def _lib():
     lib.probe_ptmi_sinf_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
     lib.probe_fp64core.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_ulonglong)]
     lib.probe_sincos_core_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
+    for name in ("probe_ptmi_noise_sinf2_all", "probe_fract_all"):
+        getattr(lib, name).argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
     lib.probe_ptmi_noise_sinf_all.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint),
                                               ctypes.POINTER(ctypes.c_ulonglong)]
     lib.probe_sinf_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
@@ -59,6 +61,31 @@ def test_kernel_noise_sinf_bit_identical_all_floats():
     assert m.value == 0, "%d mismatches, first input bits 0x%08x" % (m.value, f.value)
     n_range = 2 * (0x4E800000 - 0x49000000)  # floats with 2^19 <= |x| < 2^30, both signs
     assert fb.value == 1054, "cw30 declined %d of %d lanes (host check: 1054)" % (fb.value, n_range)
+
+
+def test_kernel_noise_sinf_pair_bit_identical_all_floats():
+    """The paired noise sin the kernels evaluate a noise3D pair with (ptmi_sinf.h noise_sinf2,
+    round 6): both outputs equal noise_sinf's (itself equal to the device library for every float,
+    above) for every float in the first slot, each paired with another float drawn from the whole bit
+    space -- every combination of reduction paths (small / Cody-Waite / Payne-Hanek band / >= 2^19)
+    of the two draws occurs."""
+    lib = _lib()
+    m, f = ctypes.c_ulonglong(), ctypes.c_uint()
+    assert lib.probe_ptmi_noise_sinf2_all(ctypes.byref(m), ctypes.byref(f)) == 0
+    assert m.value == 0, "%d mismatches, first input bits 0x%08x" % (m.value, f.value)
+
+
+def test_fract_instruction_matches_ocml_fract_all_floats():
+    """v_fract_f32 against ocml's fract (min(x - floor(x), 0x1.fffffep-1f)) on every finite float:
+    reported, and required only if the kernels use it (PTMI_R6_FRACT)."""
+    lib = _lib()
+    m, f = ctypes.c_ulonglong(), ctypes.c_uint()
+    assert lib.probe_fract_all(ctypes.byref(m), ctypes.byref(f)) == 0
+    print("v_fract_f32 vs ocml fract: %d mismatches (first 0x%08x)" % (m.value, f.value))
+    import re
+    src = open(os.path.join(os.path.dirname(__file__), "..", "pathtracer-ocl_amd", "csrc", "ptmi_kernels.hip")).read()
+    if re.search(r"#define PTMI_R6_FRACT 1", src):
+        assert m.value == 0, "the kernels use v_fract_f32 but it differs from ocml's fract"
 
 
 def test_fp64_cores_match_compiler_operators():

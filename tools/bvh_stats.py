@@ -18,7 +18,7 @@ if scene.startswith("adv:"):
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 W, H = 1280, 960
 lib = api.load_library()
-buf = (ctypes.c_ulonglong * 40)()
+buf = (ctypes.c_ulonglong * 80)()
 lib.ptmi_stats_read(buf, 1)
 objs, tris, grps, cam = scene_inputs(scene, W, H)
 api.Trace(objs, tris, grps, 0, spp, cam, seeds=layout.seeds_go_float64(W * H, 3))

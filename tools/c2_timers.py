@@ -14,7 +14,7 @@ scene = sys.argv[1] if len(sys.argv) > 1 else "reference"
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 W, H = 1280, 960
 lib = api.load_library()
-buf = (ctypes.c_ulonglong * 40)()
+buf = (ctypes.c_ulonglong * 80)()
 lib.ptmi_stats_read(buf, 1)
 objs, tris, grps, cam = scene_inputs(scene, W, H)
 api.Trace(objs, tris, grps, 0, spp, cam, seeds=layout.seeds_go_float64(W * H, 3))

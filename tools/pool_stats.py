@@ -17,7 +17,7 @@ spp = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 stride = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 W, H = 1280, 960
 lib = api.load_library()
-buf = (ctypes.c_ulonglong * 40)()
+buf = (ctypes.c_ulonglong * 80)()
 lib.ptmi_stats_read(buf, 1)
 objs, tris, grps, cam = scene_inputs(scene, W, H)
 if stride > 1:

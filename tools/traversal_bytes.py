@@ -23,7 +23,7 @@ def run(out_path, spp):
     from ptmi import api, layout
     from tests.scene_inputs import scene_inputs
     lib = api.load_library()
-    buf = (ctypes.c_ulonglong * 40)()
+    buf = (ctypes.c_ulonglong * 80)()
     res = {}
     for key, scene in CONFIGS.items():
         W, H = 1280, 960

@@ -46,7 +46,7 @@ if mode == "frame":
     torch.cuda.synchronize()
     scene.kernel_time()
     has_stats = hasattr(lib, "ptmi_stats_read")
-    buf = (ctypes.c_ulonglong * 40)()
+    buf = (ctypes.c_ulonglong * 80)()
     if has_stats:
         lib.ptmi_stats_read.restype = ctypes.c_int
         lib.ptmi_stats_read(buf, 1)
