@@ -433,9 +433,25 @@ def main():
                                        "basis": "the reference's visit rules (tracer.cl:617-719: every "
                                                 "triangle of every node whose box the line passes): the "
                                                 "bytes its traversal would fetch at this sample rate"},
-                    "fp64_reference_equivalent": fp64}
+                    # (round 5 named this "fp64_reference_equivalent") the FP64 rate
+                    # the reference's own visit rules would have to sustain at this sample rate -- a
+                    # work-equivalent figure, not the kernel's utilisation
+                    "reference_rule_work_rate": dict(fp64, bound="reference_rule_work_equivalent",
+                                                     bound_detail="FP64 flops of the reference's visit rules at "
+                                                                  "this sample rate (ptmi never executes them)")}
             if pmc and pmc.get("valu"):
                 roof["valu"] = pmc["valu"]
+        # The FP64 work the kernel actually executes (frozen PMC counters of this build, scaled to the
+        # launch), beside the algorithmic fraction roofline.frac prices: the algorithmic
+        # count credits work ptmi skips (structural zeros, the hemisphere table), the executed one is
+        # the VALU's FP64 utilisation.
+        pv = (pmc or {}).get("valu") or {}
+        if pv.get("fp64_flops_executed_per_launch"):
+            ex = pv["fp64_flops_executed_per_launch"] * share / (kms * 1e-3) / 1e12
+            roof["fp64_executed"] = {"achieved": round(ex, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                     "frac": round(ex / FP64_PEAK_TFLOPS, 4),
+                                     "basis": "rocprofv3 SQ_INSTS_VALU_{ADD,MUL,TRANS,FMA x2}_F64 x 64 x lane "
+                                              "utilisation, this build (profiles/pmc_measured.json)"}
         if pmc_note:
             roof["pmc_status"] = pmc_note
         roof.update({"build": build_id(), "traffic": None if traffic is None else round(traffic),

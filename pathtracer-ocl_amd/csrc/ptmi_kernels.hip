@@ -110,15 +110,15 @@ __shared__ unsigned long long ptmi_wstat[1][64];
 #ifndef PTMI_R6_SLOT
 #define PTMI_R6_SLOT 1  // hemisphere-table slot test: one conversion pair, no range test
 #endif
+#ifndef PTMI_R6_VACC
+#define PTMI_R6_VACC 1  // the per-pixel colour sums really in LDS (volatile slots), not promoted to VGPRs
+#endif
 #ifndef PTMI_R6_FRACT
 #define PTMI_R6_FRACT 0  // noise fract as v_fract_f32 (exhaustively checked equal to ocml's fract)
 #endif
 #ifndef PTMI_R6_NPAIR
 #define PTMI_R6_NPAIR 0  // the two draws of a noise3D pair evaluated together (ptmi_sinf.h noise_sinf2):
                          // 1 both sites, 2 camera only, 3 hemisphere only.  Measured C2 +0.6 % with 1
-#endif
-#ifndef PTMI_R6_SHLD
-#define PTMI_R6_SHLD 0  // shading: the hit object's record loads issued together, one wait
 #endif
 
 namespace ptmi {
@@ -1884,48 +1884,7 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
     d4 eye = mk(-P.rd.x, -P.rd.y, -P.rd.z, -P.rd.w);
     // Object normal -> world normal (tracer.cl:903-955).
     d4 nv;
-    // Kernels whose objects are planes and spheres only (no cylinders, cubes, meshes or textures):
-    // every record field either normal needs is loaded up front -- one wait for the lot instead
-    // of a chain of dependent loads behind the type, st and invt_diag branches -- and the
-    // scale+translate sphere normal is computed for every lane, then selected: a wave almost
-    // always holds both kinds of hit, so both were run anyway (round 6).  The arithmetic is the
-    // branchy path's (xpt with st, the diagonal inverse transpose, norm3_core); a sphere without
-    // those patterns takes the general code.
-    constexpr bool kFlat = PTMI_R6_SHLD && A && !(FL & (F_TEX | F_CYLCUBE | F_GROUPS));
-    if constexpr (kFlat) {
-        const double* R = ob.inv;
-        const double2 i0 = *reinterpret_cast<const double2*>(R + 0);    // inv[0], inv[1]
-        const double2 i2 = *reinterpret_cast<const double2*>(R + 2);    // inv[2], inv[3]
-        const double2 i4 = *reinterpret_cast<const double2*>(R + 4);    // inv[4], inv[5]
-        const double2 i6 = *reinterpret_cast<const double2*>(R + 6);    // inv[6], inv[7]
-        const double2 i10 = *reinterpret_cast<const double2*>(R + 10);  // inv[10], inv[11]
-        const double2 t0 = *reinterpret_cast<const double2*>(ob.inv_t + 0);
-        const double2 t4 = *reinterpret_cast<const double2*>(ob.inv_t + 4);
-        const double2 t10 = *reinterpret_cast<const double2*>(ob.inv_t + 10);
-        const double2 pn = *reinterpret_cast<const double2*>(ob.plane_n);
-        const double pnz = ob.plane_n[2];
-        const int2 pat = *reinterpret_cast<const int2*>(&ob.st);  // st, invt_diag
-        const bool sph = type == 1;
-        PTMI_WADD(41, 1ull);
-        // xpt (st): (m0 x + m3, m5 y + m7, m10 z + m11); on = lp - (0, 0, 0); invT diagonal
-        const d4 ns = norm3_core(mk(t0.x * (i0.x * pos.x + i2.y), t4.y * (i4.y * pos.y + i6.y),
-                                    t10.x * (i10.x * pos.z + i10.y), 0.0));
-        nv = sph ? ns : mk(pn.x, pn.y, pnz, 0.0);
-        if (sph && !(pat.x != 0 && pat.y != 0)) {
-            PTMI_WADD(42, 1ull);
-            const d4 lp = xpt<A>(ob.inv, ob.st, pos);
-            const d4 on = mk(lp.x - 0.0, lp.y - 0.0, lp.z - 0.0, 0.0);
-            const double* it = ob.inv_t;
-            d4 g;
-            if (ob.invt_diag) {
-                g = mk(it[0] * on.x, it[5] * on.y, it[10] * on.z, 0.0);
-            } else {
-                g = mk((it[0] * on.x + it[1] * on.y) + it[2] * on.z, (it[4] * on.x + it[5] * on.y) + it[6] * on.z,
-                       (it[8] * on.x + it[9] * on.y) + it[10] * on.z, 0.0);
-            }
-            nv = norm3_core(g);
-        }
-    } else if (type == 0 && !((FL & F_TEX) && ob.tex_nm)) {
+    if (type == 0 && !((FL & F_TEX) && ob.tex_nm)) {
         PTMI_WADD(41, 1ull);
         nv = ld4(ob.plane_n);  // constant per plane: normalize(mul(invT, (0,1,0,0))), w = 0
     } else {
@@ -2100,7 +2059,10 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
 
 // Per-launch resources of trace_kernel<FL>: workgroup size and the register budget.
 #ifndef PTMI_WAVES
-#define PTMI_WAVES 6  // waves/SIMD the register allocation targets (scenes without groups or materials).
+#define PTMI_WAVES 7  // waves/SIMD the register allocation targets (scenes without groups or materials).
+                      // Round 6: with the colour sums really in LDS (PTMI_R6_VACC) and the bounce-loop
+                      // cuts, C2's kernel fits 72 VGPRs without spill and C3's 72 with 16 B/lane: 7 waves,
+                      // C2 150.5 -> 145.1 ms, C3 153.0 -> 152.0 ms (profiles/r6/SUMMARY.md).  Before:
                       // With the sincos constants in SGPRs (ptmi_fp64core.h) C2/C3 fit 95 VGPRs at 5 waves
                       // without spill (C2 2048 spp 178.0 -> 171.6 ms against the old 3-wave budget); 6 waves
                       // (80 VGPRs, 64 B/lane of spilled loop invariants) gain another 2-2.6 % (C2 171.5 ->
@@ -2265,7 +2227,12 @@ __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t sample
     const XSeed seed_bits = xseed_of((uint64_t)__double_as_longlong(seed));  // statistical mode
     const uint32_t c_end = it.inside ? it.c1 : it.c0;
     auto* stk = lds_ptr(stk_lds + tid);
+#if PTMI_R6_VACC  // (the colour sums really in LDS: see trace_kernel)
+    volatile __attribute__((address_space(3))) double* acc =
+        (volatile __attribute__((address_space(3))) double*)(acc_lds + tid);
+#else
     double* acc = acc_lds + tid;
+#endif
     acc[0 * kBlock] = 0.0;
     acc[1 * kBlock] = 0.0;
     acc[2 * kBlock] = 0.0;
@@ -2520,7 +2487,15 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
         // order; they change once per path, and the registers keep the bounce loop off
         // scratch at the 6-waves/SIMD budget.
         __shared__ double acc_lds[3 * kBlock];
+        // volatile (round 6): without it the compiler, seeing no other reader, kept the three
+        // sums in registers across the whole loop -- 6 VGPRs and 3 v_mov_b64 per iteration --
+        // and wrote the LDS slots only after it.
+#if PTMI_R6_VACC
+        volatile __attribute__((address_space(3))) double* acc =
+            (volatile __attribute__((address_space(3))) double*)(acc_lds + tid);
+#else
         double* acc = acc_lds + tid;
+#endif
         acc[0 * kBlock] = 0.0;
         acc[1 * kBlock] = 0.0;
         acc[2 * kBlock] = 0.0;

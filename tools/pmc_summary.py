@@ -52,6 +52,14 @@ f64 = sum(v.get(k, 0) for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64"
 if f64 and v.get("SQ_INSTS_VALU"):
     res["fp64_share"] = f64 / v["SQ_INSTS_VALU"]
     print("FP64 share of VALU insts %.3f" % res["fp64_share"])
+    # FP64 flops the kernel executed: (ADD + MUL + TRANS + 2 FMA) wave-instructions x 64 lanes x
+    # the VALU lane utilisation (the FP64 instructions' own lane mask is not counted separately)
+    ops = sum(per(k) for k in ("SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")) + \
+        2 * per("SQ_INSTS_VALU_FMA_F64")
+    res["fp64_wave_ops_per_launch"] = ops
+    if res.get("lane_utilisation"):
+        res["fp64_flops_executed_per_launch"] = ops * 64 * res["lane_utilisation"]
+        print("FP64 flops executed / launch %.4g (lane-utilisation weighted)" % res["fp64_flops_executed_per_launch"])
 if v.get("GRBM_GUI_ACTIVE") and v.get("SQ_INSTS_VALU"):
     cyc = per("GRBM_GUI_ACTIVE") / 8.0
     res["frame_cycles"] = cyc
