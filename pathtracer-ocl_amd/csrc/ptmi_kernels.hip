@@ -114,7 +114,7 @@ __shared__ unsigned long long ptmi_wstat[1][64];
 #define PTMI_R6_VACC 1  // the per-pixel colour sums really in LDS (volatile slots), not promoted to VGPRs
 #endif
 #ifndef PTMI_R6_FRACT
-#define PTMI_R6_FRACT 0  // noise fract as v_fract_f32 (exhaustively checked equal to ocml's fract)
+#define PTMI_R6_FRACT 1  // noise fract as v_fract_f32 (exhaustively checked equal to ocml's fract)
 #endif
 #ifndef PTMI_R6_NPAIR
 #define PTMI_R6_NPAIR 0  // the two draws of a noise3D pair evaluated together (ptmi_sinf.h noise_sinf2):
@@ -340,6 +340,9 @@ __device__ __forceinline__ float noise3d(float x, float y, float z) {
 #endif
     const float sn = noise_sinf(s, [](float v) { return sinf_ocml(v); });
     float v = sn * 43758.5453f;
+    // ocml's fract: min(v - floor(v), 0x1.fffffep-1).  v_fract_f32 returns the same bits for every
+    // finite float (tests/test_gpu_rng.py, exhaustive on the GPU), in one instruction instead of three.
+    if (PTMI_R6_FRACT) return __builtin_amdgcn_fractf(v);
     return fminf(v - floorf(v), 0x1.fffffep-1f);
 }
 
@@ -365,8 +368,8 @@ __device__ __forceinline__ void noise3d_pair(float x1, float y1, float z1, float
     float sn1, sn2;
     noise_sinf2(s1, s2, [](float v) { return sinf_ocml(v); }, sn1, sn2);
     const float v1 = sn1 * 43758.5453f, v2 = sn2 * 43758.5453f;
-    u1 = fminf(v1 - floorf(v1), 0x1.fffffep-1f);
-    u2 = fminf(v2 - floorf(v2), 0x1.fffffep-1f);
+    u1 = PTMI_R6_FRACT ? __builtin_amdgcn_fractf(v1) : fminf(v1 - floorf(v1), 0x1.fffffep-1f);
+    u2 = PTMI_R6_FRACT ? __builtin_amdgcn_fractf(v2) : fminf(v2 - floorf(v2), 0x1.fffffep-1f);
 }
 
 // ---- Opt-in statistical RNG (F_XRNG, ptmi_scene_set_rng) ---------------------------
@@ -1579,21 +1582,29 @@ __device__ __forceinline__ int hemi_slot(float u) {  // table record of u, or -1
     return (t == (float)k && (unsigned)k < (unsigned)kHemiSize) ? k : -1;
 }
 
-template <bool A, bool kTab>
+// The table is two planes (round 6): [0, 2^16) the (sin, cos) pairs, [2^16, 2^17) the (sqrt u,
+// sqrt(1 - u)) pairs, 16 B per entry.  A lookup reads one 16-B entry of each plane, as before from two
+// unrelated records (u1 and u2 are independent draws); the planes let the mesh kernels keep just the
+// 1-MB (sin, cos) plane in the L2 they share with the traversal index and compute the sqrt pair
+// (kTabSqrt false): with the whole 2-MB table their HBM traffic was the table's evictions.
+#ifndef PTMI_HEMI_SQRT_GROUPS
+#define PTMI_HEMI_SQRT_GROUPS 0  // mesh kernels read the sqrt plane too (1) or compute the pair (0)
+#endif
+template <bool A, bool kTab, bool kTabSqrt = kTab>
 __device__ __forceinline__ d4 random_hemisphere(const double* __restrict__ tab, d4 nv, float u1, float u2) {
     double sr, cr, rand2s, rc;
     const int k1 = kTab ? hemi_slot(u1) : -1;
     if (k1 >= 0) {
-        const double2 q = *reinterpret_cast<const double2*>(tab + 4 * k1);
+        const double2 q = *reinterpret_cast<const double2*>(tab + 2 * k1);
         sr = q.x;
         cr = q.y;
     } else {
         PTMI_WADD(35, 1ull);
         hemi_sincos<A>(u1, sr, cr);
     }
-    const int k2 = kTab ? hemi_slot(u2) : -1;
+    const int k2 = kTabSqrt ? hemi_slot(u2) : -1;
     if (k2 >= 0) {
-        const double2 q = *reinterpret_cast<const double2*>(tab + 4 * k2 + 2);
+        const double2 q = *reinterpret_cast<const double2*>(tab + 2 * kHemiSize + 2 * k2);
         rand2s = q.x;
         rc = q.y;
     } else {
@@ -1624,7 +1635,7 @@ __global__ __launch_bounds__(256) void hemi_table_kernel(double* __restrict__ ou
     hemi_sqrt<false>(u, g[2], g[3]);
     bool same = true;
     for (int i = 0; i < 4; i++) {
-        out[4 * k + i] = a[i];
+        out[(i < 2 ? 2 * k : 2 * kHemiSize + 2 * k) + (i & 1)] = a[i];  // the two planes
         same = same && __double_as_longlong(a[i]) == __double_as_longlong(g[i]);
     }
     if (!same) atomicAdd(mismatch, 1);
@@ -1974,7 +1985,8 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
         }
         // Only affine instantiations read the table: its records are the affine sequences'
         // results, so they equal what such a lane computes by construction.
-        P.rd = random_hemisphere<A, A && (PTMI_HEMI_TAB_GROUPS || !(FL & F_GROUPS))>(S.hemi, nv, u1, u2);
+        P.rd = random_hemisphere<A, A && (PTMI_HEMI_TAB_GROUPS || !(FL & F_GROUPS)),
+                                 A && (PTMI_HEMI_SQRT_GROUPS || !(FL & F_GROUPS))>(S.hemi, nv, u1, u2);
         cosine = dotv<A>(P.rd, nv);
     }
     P.ro = over;
