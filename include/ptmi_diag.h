@@ -69,7 +69,8 @@ enum {
     PTMI_KNOB_SPLIT_SLOTS = 7,
     PTMI_KNOB_SPLIT_SYNC = 8,
     PTMI_KNOB_SPLIT_BUDGET = 9,
-    PTMI_KNOB_TAIL_SPLIT = 10
+    PTMI_KNOB_TAIL_SPLIT = 10,
+    PTMI_KNOB_MESH_ITEMS_SHARE = 11
 };
 int ptmi_diag_set_knob(ptmi_scene* s, int knob, int value);
 

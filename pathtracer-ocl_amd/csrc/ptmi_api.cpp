@@ -87,6 +87,7 @@ struct ptmi_scene {
     uint32_t tail_tiles = 0;  // chunked tiles at the end of an automatic launch; 0: default (see render)
     uint32_t tail_items = 6;  // chunk items per resident wave slot in the tail (scenes without meshes; see render)
     uint32_t mesh_items = 32;  // chunk items per resident wave slot, mesh scenes (every tile chunked)
+    uint32_t mesh_items_share = 48;  // ... in a sample-split rank's share (a sub-range of the samples)
     uint32_t min_chunk = 32;   // fewest samples per chunk item (see render)
     uint32_t tail_split = 4;   // mesh scenes: the last chunk round cut into this many (see render)
     // Mesh scenes: per-tile cost class (mesh_tile_cost) and the dispatch order built from it
@@ -437,6 +438,7 @@ int prepare_scene(const void* objects, uint32_t n_obj, const void* triangles, ui
             std::memcpy(r.row1, o.inv + 4, 32);
             r.slot = (int32_t)k;
             r.key = o.key;
+            r.nz = (r.row1[0] != 0.0 ? 1 : 0) | (r.row1[1] != 0.0 ? 2 : 0) | (r.row1[2] != 0.0 ? 4 : 0);
             hs.planes.push_back(r);
         } else if (o.type == 1 && o.st) {
             SphereRec r{};
@@ -979,7 +981,12 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         const bool mesh = (s->flags & 1) != 0;  // F_GROUPS
         if (!mesh || s->tail_tiles)
             n_tail = std::min<uint32_t>(owned_tiles, s->tail_tiles ? s->tail_tiles : (uint32_t)(s->resident_waves / 2));
-        const uint64_t want = (uint64_t)s->resident_waves * (mesh ? s->mesh_items : s->tail_items);
+        // A sample-split rank (a sub-range of the samples, every tile) of a mesh scene: 48 items per
+        // slot instead of 32 (round 6, C4 8 ranks: projected efficiency 0.896 -> 0.911; the one-GPU
+        // plan keeps 32: 48 cost its frame 1.7 %).  Tile-split ranks keep 32 (C5: 0.857 / 0.854).
+        const bool sample_share = mesh && tile_stride == 1 && range < samples;
+        const uint64_t want =
+            (uint64_t)s->resident_waves * (mesh ? (sample_share ? s->mesh_items_share : s->mesh_items) : s->tail_items);
         // A mesh scene's tile-split rank owns 1/N of the tiles, so a chunk round is a fraction
         // of the machine (2,400 items at N = 8 against 4,096 wave slots) and the 64-sample floor
         // held it at ~19 items per slot; half the floor lets the items-per-slot target bind
@@ -1262,10 +1269,11 @@ int ptmi_trace(const void* objects, uint32_t n_obj, const void* triangles, uint3
 
 // Sample split by cost, not count: the first sample index of device g of n (g = n ->
 // samples).  Samples past n ~ 553 / ~731 put the hemisphere / anti-aliasing noise on
-// the large-argument sin reduction and cost ~2 / ~4 % more (x50 weights 50, 51, 52).
-// Same table as ptmi/dist.py's sample_split_point.
+// the large-argument sin reduction and cost ~1 / ~2 % more (x100 weights 100, 101, 102; round 6,
+// re-measured on the round-6 kernel's 8-rank shares -- round 5's 50 / 51 / 52 left rank 0 2.5 %
+// over the mean).  Same table as ptmi/dist.py's sample_split_point.
 static uint32_t split_point(int g, int n, uint32_t samples) {
-    static const uint64_t knot[2] = {553, 731}, w[3] = {50, 51, 52};
+    static const uint64_t knot[2] = {553, 731}, w[3] = {100, 101, 102};
     auto cost = [&](uint64_t m) {
         return w[0] * std::min<uint64_t>(m, knot[0]) + w[1] * (std::min<uint64_t>(std::max<uint64_t>(m, knot[0]), knot[1]) - knot[0]) +
                w[2] * (std::max<uint64_t>(m, knot[1]) - knot[1]);
@@ -1595,6 +1603,7 @@ extern "C" int ptmi_diag_set_knob(ptmi_scene* s, int knob, int value) {
     case PTMI_KNOB_TAIL_TILES: s->tail_tiles = (uint32_t)std::max(0, value); return PTMI_OK;
     case PTMI_KNOB_TAIL_ITEMS: s->tail_items = pos; return PTMI_OK;
     case PTMI_KNOB_MESH_ITEMS: s->mesh_items = pos; return PTMI_OK;
+    case PTMI_KNOB_MESH_ITEMS_SHARE: s->mesh_items_share = pos; return PTMI_OK;
     case PTMI_KNOB_MIN_CHUNK: s->min_chunk = pos; return PTMI_OK;
     case PTMI_KNOB_TAIL_SPLIT: s->tail_split = pos; return PTMI_OK;
     case PTMI_KNOB_TILE_ORDER:

@@ -140,7 +140,7 @@ struct alignas(16) PlaneRec {  // intersectPlane needs row 1 of the inverse only
     double row1[4];
     int32_t slot, key;  // DevScene::objs slot, reference list index
     int32_t par;        // affine pairing (find_closest_prims): the next plane has the same row1[0..2]
-    int32_t pad;
+    int32_t nz;         // bit i set: row1[i] (i < 3) is not +-0 (the affine kernels skip +-0 terms)
 };
 struct alignas(16) SphereRec {  // sphere with the scale+translate inverse pattern
     double m0, m3, m5, m7, m10, m11, m15, pad;

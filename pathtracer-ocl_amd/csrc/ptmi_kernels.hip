@@ -110,6 +110,10 @@ __shared__ unsigned long long ptmi_wstat[1][64];
 #ifndef PTMI_R6_SLOT
 #define PTMI_R6_SLOT 1  // hemisphere-table slot test: one conversion pair, no range test
 #endif
+#ifndef PTMI_R6_PLNZ
+#define PTMI_R6_PLNZ 0  // affine planes past the floor / ceiling run: +-0 row entries skipped by pattern
+                        // (measured slower: C2 +0.8 %, C3 +2.3 %, profiles/r6/SUMMARY.md)
+#endif
 #ifndef PTMI_R6_VACC
 #define PTMI_R6_VACC 1  // the per-pixel colour sums really in LDS (volatile slots), not promoted to VGPRs
 #endif
@@ -1252,12 +1256,44 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
             plane_take(P1, q1, k1);
         }
     }
+    // Affine planes after the floor / ceiling run: the +-0 entries of row1[0..2] skipped by their
+    // pattern (PlaneRec::nz, a uniform switch; round 6): walls rotated about one axis keep one exact
+    // zero (the reference scene's side walls (x, y), its back wall (y, z)).  Same terms in the same
+    // order, so the sums are bit-identical up to the sign of an exact zero (plane_rows_nz).
+    auto sum_nz = [&](auto nzc, const auto* m, double x, double y, double z) {
+        constexpr int NZ = decltype(nzc)::value;
+        double o = 0.0;
+        bool any = false;
+        if constexpr ((NZ & 1) != 0) {
+            o = m[0] * x;
+            any = true;
+        }
+        if constexpr ((NZ & 2) != 0) {
+            o = any ? o + m[1] * y : m[1] * y;
+            any = true;
+        }
+        if constexpr ((NZ & 4) != 0) o = any ? o + m[2] * z : m[2] * z;
+        return o;
+    };
+    auto par_pair = [&](auto nzc, const auto& P0, const auto& P1, double& q0, bool& k0, double& q1, bool& k1) {
+        const auto* m = P0.row1;
+        const double a = sum_nz(nzc, m, ro.x, ro.y, ro.z);
+        const double dy = sum_nz(nzc, m, rd.x, rd.y, rd.z);
+        plane_q2(a + m[3], a + P1.row1[3], dy, q0, k0, q1, k1);
+    };
     for (; p + 1 < np; p += 2) {
         PTMI_WADD(48, 1ull);
         const auto &P0 = cmem(S.planes)[p], &P1 = cmem(S.planes)[p + 1];
         double oy0, dy0, oy1, dy1, q0, q1;
         bool k0, k1;
-        if (A && P0.par) {  // parallel pair: one sum of the origin's x, y, z terms, one direction term
+        if (A && P0.par && PTMI_R6_PLNZ) {
+            switch (P0.nz) {
+                case 3: par_pair(std::integral_constant<int, 3>(), P0, P1, q0, k0, q1, k1); break;
+                case 5: par_pair(std::integral_constant<int, 5>(), P0, P1, q0, k0, q1, k1); break;
+                case 6: par_pair(std::integral_constant<int, 6>(), P0, P1, q0, k0, q1, k1); break;
+                default: par_pair(std::integral_constant<int, 7>(), P0, P1, q0, k0, q1, k1); break;
+            }
+        } else if (A && P0.par) {  // parallel pair: one sum of the origin's x, y, z terms, one direction term
             const auto* m = P0.row1;  // and one reciprocal (row1[0..2] of P1 are the same bits)
             const double a = (m[0] * ro.x + m[1] * ro.y) + m[2] * ro.z;
             oy0 = a + m[3];
@@ -1278,7 +1314,18 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         const auto& P0 = cmem(S.planes)[p];
         double q0;
         bool k0;
-        plane_t(P0, q0, k0);
+        if (A && PTMI_R6_PLNZ) {
+            double oy, dy;
+            switch (P0.nz) {
+                case 3: plane_rows_nz<3>(P0.row1, ro, rd, oy, dy); break;
+                case 5: plane_rows_nz<5>(P0.row1, ro, rd, oy, dy); break;
+                case 6: plane_rows_nz<6>(P0.row1, ro, rd, oy, dy); break;
+                default: plane_rows(P0, oy, dy); break;
+            }
+            plane_q(oy, dy, q0, k0);
+        } else {
+            plane_t(P0, q0, k0);
+        }
         plane_take(P0, q0, k0);
     }
     const int nq = (PTMI_ABLATE & 16) ? 0 : S.n_spheres_st;
@@ -1325,6 +1372,15 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         pend = disc > 0.0;
     };
     int q = 0;
+    if (PTMI_R6_SPH && nq == 1) {
+        const auto& Q0 = cmem(S.spheres)[0];
+        d4 o0, d0;
+        sphere_ray(Q0, o0, d0);
+        double a0, b0, disc0;
+        sphere_quad<A>(o0, d0, a0, b0, disc0);
+        first(a0, b0, disc0, Q0.slot, Q0.key);
+        q = 1;
+    }
     if (PTMI_R6_SPH && nq >= 2) {
         PTMI_WADD(50, 1ull);
         const auto &Q0 = cmem(S.spheres)[0], &Q1 = cmem(S.spheres)[1];
@@ -1357,8 +1413,7 @@ __device__ __forceinline__ Hit find_closest_prims(const DevScene& S, d4 ro, d4 r
         sphere_ray(Q0, o0, d0);
         double a0, b0, disc0;
         sphere_quad<A>(o0, d0, a0, b0, disc0);
-        if (PTMI_R6_SPH && q == 0) first(a0, b0, disc0, Q0.slot, Q0.key);
-        else defer(a0, b0, disc0, Q0.slot, Q0.key);
+        defer(a0, b0, disc0, Q0.slot, Q0.key);  // (q >= 2 here when PTMI_R6_SPH: the first sphere is peeled)
     }
     if (pend) {
         PTMI_WADD(33, 1ull);

@@ -23,13 +23,14 @@ differs from a one-GPU render only by FP64 summation order (~1e-16 relative).
 """
 TILE = 8  # ptmi_device.h kTile
 
-# Relative cost of one sample by its index n (x50): past n ~ 553 the hemisphere noise
+# Relative cost of one sample by its index n (x100): past n ~ 553 the hemisphere noise
 # arguments (n * 237.212 + ...) and past ~731 the anti-aliasing ones (n * 179.233)
-# reach 2^17, ocml's large-argument sin reduction (csrc/ptmi_sinf.h).  Measured on
-# C2 (tools/sample_cost.py): 256-sample slices take 23.5 ms below n = 512 and 24.5 ms
-# above 768.  Same table as ptmi_api.cpp's split_point.
-_COST_KNOTS = ((553, 50), (731, 51))
-_COST_TAIL = 52
+# reach 2^17, ocml's large-argument sin reduction (csrc/ptmi_sinf.h).  Round 6, the
+# round-6 kernel's 8-rank C2 shares (tools/shard_balance.py): 0.0704 ms per sample of
+# the frame below n = 553 and 0.0718 past 731 (round 5: x50 weights 50, 51, 52 from
+# 256-sample slices of 23.5 / 24.5 ms).  Same table as ptmi_api.cpp's split_point.
+_COST_KNOTS = ((553, 100), (731, 101))
+_COST_TAIL = 102
 
 
 def _cost(n):
