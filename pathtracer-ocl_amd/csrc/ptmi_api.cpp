@@ -981,10 +981,11 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         const bool mesh = (s->flags & 1) != 0;  // F_GROUPS
         if (!mesh || s->tail_tiles)
             n_tail = std::min<uint32_t>(owned_tiles, s->tail_tiles ? s->tail_tiles : (uint32_t)(s->resident_waves / 2));
-        // A sample-split rank (a sub-range of the samples, every tile) of a mesh scene: 48 items per
-        // slot instead of 32 (round 6, C4 8 ranks: projected efficiency 0.896 -> 0.911; the one-GPU
-        // plan keeps 32: 48 cost its frame 1.7 %).  Tile-split ranks keep 32 (C5: 0.857 / 0.854).
-        const bool sample_share = mesh && tile_stride == 1 && range < samples;
+        // A sample-split rank of a mesh scene holding at most a quarter of the samples (every tile):
+        // 48 items per slot instead of 32 (round 6, C4 8 ranks: projected efficiency 0.896 -> 0.904;
+        // at 2 ranks 48 cost 0.962 -> 0.940, and the one-GPU frame 1.7 %, so those keep 32).
+        // Tile-split ranks keep 32 (C5: 0.857 / 0.854).
+        const bool sample_share = mesh && tile_stride == 1 && (uint64_t)range * 4 <= samples;
         const uint64_t want =
             (uint64_t)s->resident_waves * (mesh ? (sample_share ? s->mesh_items_share : s->mesh_items) : s->tail_items);
         // A mesh scene's tile-split rank owns 1/N of the tiles, so a chunk round is a fraction
