@@ -122,7 +122,8 @@ __shared__ unsigned long long ptmi_wstat[1][64];
 #endif
 #ifndef PTMI_R6_NPAIR
 #define PTMI_R6_NPAIR 0  // the two draws of a noise3D pair evaluated together (ptmi_sinf.h noise_sinf2):
-                         // 1 both sites, 2 camera only, 3 hemisphere only.  Measured C2 +0.6 % with 1
+                         // 1 both sites, 2 camera only, 3 hemisphere only.  Measured slower, C2 +0.6 / +0.3 /
+                         // +0.5 % (its two interleaved chains hold more registers at the peak)
 #endif
 
 namespace ptmi {
