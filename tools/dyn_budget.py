@@ -88,13 +88,14 @@ def subphase(chain, fr, src_lines, fp):
     noise = any(f == "ptmi_sinf.h" for f, _ in chain) or in_fn("noise3d")
     if noise:
         site = "camera" if in_fn("camera_offsets") else "shading"
-        if line_in("ptmi_sinf.h", 59, 67):
+        sr = sinf_ranges()
+        if line_in("ptmi_sinf.h", *sr["small"]):
             sub = "small"
-        elif line_in("ptmi_sinf.h", 71, 93):
+        elif line_in("ptmi_sinf.h", *sr["cw64"]) or line_in("ptmi_sinf.h", *sr["cw64_fn"]):
             sub = "cw64"
-        elif line_in("ptmi_sinf.h", 94, 146):
+        elif line_in("ptmi_sinf.h", *sr["payne_hanek"]):
             sub = "payne_hanek"
-        elif line_in("ptmi_sinf.h", 180, 206) or line_in("ptmi_sinf.h", 218, 220):
+        elif line_in("ptmi_sinf.h", *sr["cw30"]):
             sub = "ge_2^19"
         else:
             sub = "common"
@@ -126,14 +127,35 @@ def subphase(chain, fr, src_lines, fp):
             if f == fp and a <= ln <= b:
                 txt = src_lines[ln - 1]
                 blk = shade_blocks(src_lines, a, b)
-                for name, (x0, x1) in blk.items():
-                    if x0 <= ln <= x1:
+                for name, (x0, x1) in sorted(blk.items(), key=lambda kv: kv[1][1] - kv[1][0]):
+                    if x0 <= ln <= x1:  # innermost (smallest) block first
                         return "shading", name
         return "shading", "common"
     return "loop", "loop"
 
 
 _blk_cache = {}
+
+
+def sinf_ranges():
+    """Line ranges in ptmi_sinf.h of the noise sin's paths: the small-argument reduction, the FP64
+    Cody-Waite block of sf_redux_large_17_19 (and sf_cw64), its Payne-Hanek rest, sinf_cw30."""
+    if "sinf" in _blk_cache:
+        return _blk_cache["sinf"]
+    import isa_budget as ib
+    path = os.path.join(ib.CSRC, "ptmi_sinf.h")
+    lines = open(path).read().split("\n")
+    fr = {}
+    for i, l in enumerate(lines):
+        m = re.match(r"^PTMI_SINF_FN\s.*?\b(\w+)\s*\(", l)
+        if m:
+            fr[m.group(1)] = (i + 1, _close(lines, i, len(lines)))
+    a, b = fr["sf_redux_large_17_19"]
+    cw_end = next(i + 1 for i in range(a, b) if lines[i].startswith("#endif"))
+    res = {"small": fr["sf_redux_small"], "cw64": (a, cw_end), "payne_hanek": (cw_end + 1, b),
+           "cw30": fr["sinf_cw30"], "cw64_fn": fr.get("sf_cw64", (0, -1))}
+    _blk_cache["sinf"] = res
+    return res
 
 
 def _close(src_lines, start, limit):
@@ -160,7 +182,8 @@ def prims_blocks(src_lines, fcp):
     marks = {"plane_ypair": "for (; p + 1 < npy; p += 2)", "plane_pair": "for (; p + 1 < np; p += 2)",
              "plane_single": "if (p < np) {", "sphere_first_pair": "if (PTMI_R6_SPH && nq >= 2) {",
              "sphere_pair": "for (; q + 1 < nq; q += 2)", "sphere_single": "if (q < nq) {",
-             "sphere_roots_call": "if (pend) {", "sphere_general": "for (; j < S.run_end[1]; j++) {"}
+             "sphere_roots_call": "if (pend) {", "sphere_general": "for (; j < S.run_end[1]; j++) {",
+             "sphere_first_single": "if (PTMI_R6_SPH && nq == 1) {"}
     res = {}
     for i in range(fcp[0] - 1, fcp[1]):
         for name, m in marks.items():
@@ -199,6 +222,8 @@ def shade_blocks(src_lines, a, b):
             res["other_normal"] = (e, block_from(e - 1, src_lines[e - 1].index("else")))
         if "if (er > 0.0) {" in t and "emission" not in res:
             res["emission"] = (i + 1, block_from(i))
+        if "// group: interpolated vertex normal" in t and "normal_group" not in res:
+            res["normal_group"] = (i + 1, block_from(i))
     _blk_cache[key] = res
     return res
 
@@ -256,6 +281,9 @@ def static_table(fl, extra):
 
 
 # wave-level executions of each sub-phase from the stats counters (see the module docstring)
+counts_fl_no_groups = True  # (table: set from --fl: kernels without F_GROUPS)
+
+
 def executions(v):
     draws = max(v[40], 1)
     cam_draws = 2 * v[32]
@@ -267,6 +295,10 @@ def executions(v):
          ("spheres", "sphere_pair"): v[51], ("spheres", "sphere_single"): v[52],
          ("spheres", "sphere_roots_call"): v[33], ("spheres", "roots_deferred"): v[33],
          ("spheres", "sphere_general"): v[53],
+         # the one-sphere peel runs only when the scene has exactly one such sphere
+         ("spheres", "sphere_first_single"): v[45] if (v[50] == 0 and v[52] > 0) else 0,
+         # the mesh triangle's normal: never in a kernel without groups (the C2 / C3 tables)
+         ("shading", "normal_group"): 0 if counts_fl_no_groups else v[42],
          ("spheres", "roots_inplace"): v[34], ("hemisphere", "table_basis"): v[44],
          ("hemisphere", "sincos_fallback"): v[35], ("hemisphere", "sqrt_fallback"): v[36],
          ("shading", "common"): v[44], ("shading", "plane_normal"): v[41],
@@ -298,6 +330,8 @@ def main():
     if len(args) > 1 and args[1].endswith(".json"):
         counts = json.load(open(args[1]))
     fl = int(args[args.index("--fl") + 1]) if "--fl" in args else 0
+    global counts_fl_no_groups
+    counts_fl_no_groups = (fl & 1) == 0
     measured = float(args[args.index("--measured") + 1]) if "--measured" in args else None
     extra = [a for a in args if a.startswith("-D")]
     tab = static_table(fl, extra)
