@@ -1118,7 +1118,7 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         }
     }
     if (tile_stride > 1) HIP_TRY(hipMemsetAsync(sums_dev, 0, (size_t)npix * 4 * sizeof(double), st));  // un-owned tiles
-    const bool planes = (s->flags & 1) == 0;  // partial layout (ptmi_kernels.hip store_sums): planes without meshes
+    const bool planes = (s->flags & 1) == 0 || (PTMI_MESH_PLANES && !split);  // partial layout (ptmi_kernels.hip store_sums)
     const size_t need = (size_t)wp.n_tail * 64 * chunks * (planes ? 3 : 4) * sizeof(double);
     if (need > s->partial_bytes) {
         if (s->partial) {

@@ -228,6 +228,12 @@ constexpr uint32_t kSlotFree = 0xFFFFFFFFu, kSlotDead = 0xFFFFFFFEu;
 
 constexpr int kTile = 8;          // a wave64 covers an 8x8 pixel tile
 
+// Chunk partials of the mesh kernels as r, g, b planes, as the kernels without meshes store
+// them, instead of (r, g, b, samples) records (ptmi_kernels.hip store_sums; round 6).
+#ifndef PTMI_MESH_PLANES
+#define PTMI_MESH_PLANES 1
+#endif
+
 // One launch's work items (trace_kernel, by value).  The owned tiles are
 // tile_offset + k * tile_stride, k = 0, 1, ... (or tiles[k], see below)  The first n_whole of them are one
 // item each over the whole sample range [s_begin, s_end), summed straight into the

@@ -2200,28 +2200,50 @@ __device__ __forceinline__ Item work_item(const DevScene& S, const WorkPlan& WP,
 }
 
 // A whole-tile item writes its pixel's (r, g, b, samples) into the frame sums.  A chunk
-// item: kPlanes (scenes without meshes), its r, g, b into plane k of the partial buffer
-// at k * (nchunks * n_tail * 64) + oslot, the sample counts re-derived by
-// reduce_chunks_kernel (24 B per lane and item); else the same (r, g, b, samples) record
-// as a whole tile.  The register allocation of both kernels is sensitive to this
-// epilogue: the plane store costs the mesh kernels 9 more spill reloads in the loop
-// (C4/C5 +2 %), the row layout ([(item * 3 + k) * 64 + lane]) C2 +0.3 %.
+// item: kPlanes, its r, g, b into plane k of the partial buffer at
+// k * (nchunks * n_tail * 64) + oslot, the sample counts re-derived by reduce_chunks_kernel
+// (24 B per lane and item); else the same (r, g, b, samples) record as a whole tile.  The
+// stores are non-temporal: written once, read by the reduce after the launch, they should not
+// evict the mesh index and the hemisphere table from an XCD's L2.
+// Round 3 kept the mesh kernels on records (the plane store then cost them 9 more spill
+// reloads in the loop, C4/C5 +2 %; the row layout [(item * 3 + k) * 64 + lane] cost C2
+// +0.3 %).  Round 6, where the mesh kernel stores after its loop from a re-derived item:
+// planes C4 533.4 / 532.6 -> 529.7 / 531.1 ms, C5 828.5 / 826.8 -> 823.0 / 824.8; planes and
+// non-temporal stores 528.9 / 530.8 and 822.2 / 825.5 ms, C2 unchanged (145.2 / 145.0 ->
+// 145.2 / 145.1); HBM per launch C4 1.05 -> 0.88 GB, C5 3.71 -> 3.36 GB (profiles/r6/traffic).
+#ifndef PTMI_NT_SUMS
+#define PTMI_NT_SUMS 1
+#endif
 template <bool kPlanes>
 __device__ __forceinline__ void store_sums(const Item& it, const WorkPlan& WP, double* __restrict__ sums,
                                            double* __restrict__ part, double cr, double cg, double cb) {
     if (!it.inside) return;
     if (kPlanes && !it.whole) {
         const size_t plane = (size_t)WP.nchunks * WP.n_tail * 64;
+        if (PTMI_NT_SUMS) {
+            __builtin_nontemporal_store(cr, part + it.oslot);
+            __builtin_nontemporal_store(cg, part + plane + it.oslot);
+            __builtin_nontemporal_store(cb, part + 2 * plane + it.oslot);
+            return;
+        }
         part[it.oslot] = cr;
         part[plane + it.oslot] = cg;
         part[2 * plane + it.oslot] = cb;
         return;
     }
     double* o = (it.whole ? sums : part) + it.oslot * 4;
+    const double ns = (double)(it.c1 > it.c0 ? it.c1 - it.c0 : 0);
+    if (PTMI_NT_SUMS) {
+        __builtin_nontemporal_store(cr, o + 0);
+        __builtin_nontemporal_store(cg, o + 1);
+        __builtin_nontemporal_store(cb, o + 2);
+        __builtin_nontemporal_store(ns, o + 3);
+        return;
+    }
     o[0] = cr;
     o[1] = cg;
     o[2] = cb;
-    o[3] = (double)(it.c1 > it.c0 ? it.c1 - it.c0 : 0);
+    o[3] = ns;
 }
 
 // The scene record through an opaque uniform pointer to the kernel's arguments (DevScene is
@@ -2460,7 +2482,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t sample
 #endif
     // The work item is re-derived (a few integer operations) rather than kept live across
     // the loop: its fields would hold ~5 VGPRs through every walk phase.
-    store_sums<false>(work_item<(FL & F_TLIST) != 0>(S, WP, item, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
+    store_sums<PTMI_MESH_PLANES != 0>(work_item<(FL & F_TLIST) != 0>(S, WP, item, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
 }
 
 // Per-item duration onto its tile's cost accumulator (WorkPlan::cost, tile_order_kernel;
