@@ -998,6 +998,8 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
         chunks = (uint32_t)std::min<uint64_t>((want + n_tail - 1) / std::max<uint32_t>(n_tail, 1),
                                               std::max<uint32_t>(range / floor, 1));
     }
+    // The path pool of the tile-list kernels numbers an item's paths 64 x its samples in 32 bits.
+    if (tlist) chunks = std::max<uint32_t>(chunks, (range + (1u << 25) - 1) >> 25);
     chunks = std::max<uint32_t>(1, std::min<uint32_t>(chunks, std::max<uint32_t>(range, 1)));
     const uint32_t chunk_len = range == 0 ? 1 : (range + chunks - 1) / chunks;
     chunks = range == 0 ? 1 : (range + chunk_len - 1) / chunk_len;

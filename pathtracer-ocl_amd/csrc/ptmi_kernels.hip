@@ -2275,6 +2275,30 @@ __device__ __forceinline__ const DevScene& scene_reload(const DevScene& S) {
 // rays that reach a mesh in any one bounce.  Each lane still traces its samples in
 // order, and the closest hit does not depend on when or in which order candidates are
 // examined (lexicographic minimum, better()).
+// Path pool (round 6; every affine narrow-code mesh kernel, i.e. trace_kernel<1|3|5|...> and the
+// F_TLIST ones).  A mesh work item is one tile's chunk of samples, lane t tracing pixel t's samples
+// in order, so a lane that has traced its chunk idled until the wave's slowest lane was done: 5.7 %
+// of the one-GPU loop lane-cycles and 12-15 % of an 8-rank tile share's, whose chunks are short
+// (C5 at N = 8: 55 chunks of 38 samples; profiles/r5/timeline).  With the pool a wave's lanes take
+// the item's (pixel, sample) paths in order from one wave-wide counter -- path j is pixel j mod 64,
+// sample c0 + j / 64 -- whenever their camera buffer is empty, idle lanes first, so no lane idles
+// before the item's last 64 paths.  Every path is the reference's path of its (pixel, sample), bit
+// for bit; a pixel's colour sum adds its paths in completion order (LDS atomic adds, ds_add_f64)
+// instead of sample order: an FP64 summation-order difference (~1e-16 relative), deterministic (one
+// wave runs the item in lock step) and independent of the item's tile list or dispatch.  The loop
+// carries the buffered path's id instead of the lane's pixel, seed values and sample counter; fgi
+// is read from a per-tile LDS table at shading, fgi2 recomputed from the seed at the camera refill,
+// and the traversal stack takes the 21 entries the index's depth bound needs (ptmi_bvh.cpp), so the
+// LDS stays at 16 waves per CU (10,112 B per wave); spill 48 -> 16 B/lane (trace_kernel<5>).
+// 2048 spp, one MI355X, same box (profiles/r6/pool): C4 528.3 -> 489.8 ms, C5 822.9 -> 784.3 ms;
+// 8-rank shares (tools/shard_balance.py): C5 tile split Sigma/T1 1.195 -> 1.050, projected
+// efficiency 0.831 -> 0.941.  (The generic, wide-code and statistical-RNG mesh kernels keep
+// trace_groups; PTMI_POOL=0 builds the diagnostic libraries without the pool.)
+#ifndef PTMI_POOL
+#define PTMI_POOL 1
+#endif
+template <int FL>
+constexpr bool kPoolOf = PTMI_POOL != 0 && (FL & F_GROUPS) != 0 && !(FL & (F_PROJ | F_WIDE | F_XRNG));
 template <int FL>
 __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t samples, const WorkPlan& WP,
                                              const double* __restrict__ seeds, const double* __restrict__ sunf,
@@ -2485,6 +2509,157 @@ __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t sample
     store_sums<PTMI_MESH_PLANES != 0>(work_item<(FL & F_TLIST) != 0>(S, WP, item, lane), WP, sums, part, acc[0 * kBlock], acc[1 * kBlock], acc[2 * kBlock]);
 }
 
+// trace_groups with the path pool (kPoolOf above): the same loop, phases and walks; what
+// changes is which (pixel, sample) a lane's next camera ray is for, and where its colour goes.
+template <int FL>
+__device__ __forceinline__ void trace_groups_pool(const DevScene& S0, uint32_t samples, const WorkPlan& WP,
+                                                  const double* __restrict__ seeds, const double* __restrict__ sunf,
+                                                  double* __restrict__ sums, double* __restrict__ part,
+                                                  uint32_t item) {
+    constexpr bool A = true;
+    constexpr bool kDof = (FL & F_DOF) != 0;
+    constexpr int kCamComp = kDof ? 6 : 3;
+    constexpr int kPoolStack = 21;  // ptmi_bvh.cpp kMaxNode4Depth * 3
+    static_assert(kPoolStack <= kStack, "pool stack");
+    __shared__ StackEntry<true> stk_lds[kPoolStack * kStkStride];
+    __shared__ double acc_lds[3 * kBlock];  // colour sum of pixel t of the tile at [k * 64 + t]
+    __shared__ double acm_lds[3 * kBlock];  // accumColor / mask of the lane's path (as trace_groups)
+    __shared__ double msk_lds[3 * kBlock];
+    __shared__ double hp_t_lds[kBlock];
+    __shared__ int hp_pk_lds[kBlock];
+    __shared__ double cam_lds[kCamComp * kBlock];
+    __shared__ uint32_t ncur_lds[kBlock];  // the lane's current path j: pixel j & 63, sample c0 + (j >> 6)
+    __shared__ float fgi_lds[kBlock];      // fgi of pixel t of the tile
+    const int tid = threadIdx.x, lane = tid & 63;
+#if PTMI_STATS
+    ptmi_wstat[0][lane] = 0;
+#endif
+    const Item it = work_item<(FL & F_TLIST) != 0>(S0, WP, item, lane);
+    if (!it.ok) return;
+    const double seed0 = it.inside ? seeds[it.i] : 0.0;
+    fgi_lds[tid] = (float)(seed0 / (double)S0.n_list);
+    acc_lds[0 * kBlock + tid] = 0.0;
+    acc_lds[1 * kBlock + tid] = 0.0;
+    acc_lds[2 * kBlock + tid] = 0.0;
+    // The tile's origin and sample range are the wave's (work_item of lane 0).
+    const int tx0 = __builtin_amdgcn_readfirstlane(it.px - (lane & 7));
+    const int ty0 = __builtin_amdgcn_readfirstlane(it.py - (lane >> 3));
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)it.c0);
+    const uint32_t total = 64u * ((uint32_t)__builtin_amdgcn_readfirstlane((int)it.c1) - c0);
+    const int W = S0.cam.width, H = S0.cam.height;
+    auto* stk = lds_ptr(stk_lds + tid);
+    double* acm = acm_lds + tid;
+    double* msk = msk_lds + tid;
+    uint32_t j_next = 0;  // the next path of the item (wave-uniform)
+    uint32_t buf_id = 0;  // the buffered camera ray's path j
+    bool buffered = false, active = false, pending = false;
+    PathState P;
+    for (;;) {
+        if (!__any(active || buffered) && j_next >= total) break;
+        const DevScene& S = scene_reload<(PTMI_SCENE_RELOAD & 1) != 0>(S0);
+        // Camera rays in wave-wide batches, as trace_groups; the lanes without a buffered ray take
+        // the next paths, idle lanes first.
+        const uint32_t avail = total - j_next;
+        const uint64_t m_idle = __ballot(!buffered && !active), m_busy = __ballot(!buffered && active);
+        const uint32_t n_idle = min((uint32_t)__popcll(m_idle), avail);
+        const uint32_t n_need = min((uint32_t)(__popcll(m_idle) + __popcll(m_busy)), avail);
+        if (n_need >= (uint32_t)kRefillNeed || n_idle >= (uint32_t)PTMI_REFILL_STARVE_GROUPS ||
+            (n_idle > 0 && !__any(active))) {
+            const uint32_t rank = active ? (uint32_t)__popcll(m_idle) + __builtin_amdgcn_mbcnt_hi(
+                                                                            (uint32_t)(m_busy >> 32),
+                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m_busy, 0u))
+                                         : __builtin_amdgcn_mbcnt_hi((uint32_t)(m_idle >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m_idle, 0u));
+            if (!buffered && rank < avail) {
+                const uint32_t j = j_next + rank;
+                const uint32_t p = j & 63u, n = c0 + (j >> 6);
+                const int px = tx0 + (int)(p & 7u), py = ty0 + (int)(p >> 3);
+                const bool in = px < W && py < H;
+                const double sd = in ? seeds[(uint32_t)py * (uint32_t)W + (uint32_t)px] : 0.0;
+                const float fgi2 = (float)(sd / (double)samples);
+                const DevCamera& cam = camera_ptr<(PTMI_CAM_RELOAD & 2) != 0>(S);
+                d4 ro, rd;
+                float rx, ry;
+                camera_offsets<FL>(fgi_lds[p], fgi2, XSeed{}, n, rx, ry);
+                ray_for_pixel<kDof, A>(cam, sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n, ro, rd);
+                double* cb = cam_lds + tid;
+                cb[0 * kBlock] = rd.x;
+                cb[1 * kBlock] = rd.y;
+                cb[2 * kBlock] = rd.z;
+                if constexpr (kCamComp > 3) {
+                    cb[3 * kBlock] = ro.x;
+                    cb[4 * kBlock] = ro.y;
+                    cb[5 * kBlock] = ro.z;
+                }
+                buf_id = j;
+                buffered = true;
+            }
+            j_next += n_need;
+        }
+        if (!active && buffered) {
+            const double* cb = cam_lds + tid;
+            const d4 crd = mk(cb[0 * kBlock], cb[1 * kBlock], cb[2 * kBlock], 0.0);
+            d4 cro;
+            if constexpr (kCamComp > 3) {
+                cro = mk(cb[3 * kBlock], cb[4 * kBlock], cb[5 * kBlock], 1.0);
+            } else {
+                const double* co = camera_ptr<(PTMI_CAM_RELOAD & 2) != 0>(S).origin;
+                cro = mk(co[0], co[1], co[2], 1.0);
+            }
+            start_path<A, kDof>(P, cro, crd);
+            acm[0 * kBlock] = 0.0;
+            acm[1 * kBlock] = 0.0;
+            acm[2 * kBlock] = 0.0;
+            msk[0 * kBlock] = 1.0;
+            msk[1 * kBlock] = 1.0;
+            msk[2 * kBlock] = 1.0;
+            ncur_lds[tid] = buf_id;
+            buffered = false;
+            active = true;
+        }
+        bool ready = false;
+        Hit h;
+        if (active && !pending) {
+            if (P.dead) {
+                h.pk = -1;
+                ready = true;
+            } else {
+                h = find_closest_prims<FL>(S, P.ro, P.rd);
+                if (group_needs_walk<A>(S, P.ro, P.rd, h)) {
+                    pending = true;
+                    hp_t_lds[tid] = h.t;
+                    hp_pk_lds[tid] = h.pk;
+                } else {
+                    ready = true;
+                }
+            }
+        }
+        const int n_pend = __popcll(__ballot(pending));
+        if (n_pend >= kWalkBatch || (n_pend > 0 && !__any(ready))) {
+            if (pending) {
+                h = Hit{hp_t_lds[tid], hp_pk_lds[tid], -1, -1, 0.0, 0.0};
+                group_walks<A>(S, stk, P.ro, P.rd, h);
+                pending = false;
+                ready = true;
+            }
+        }
+        if (ready) {
+            const uint32_t id = ncur_lds[tid];
+            if (bounce_shade<FL, true, true>(S, P, h, fgi_lds[id & 63u], c0 + (id >> 6), acm, msk)) {
+                // colors += accumColor (tracer.cl:1179) into the path's pixel; two lanes may finish
+                // paths of one pixel in the same step, hence the atomic adds.
+                const uint32_t p = id & 63u;
+                atomicAdd(&acc_lds[0 * kBlock + p], acm[0 * kBlock]);
+                atomicAdd(&acc_lds[1 * kBlock + p], acm[1 * kBlock]);
+                atomicAdd(&acc_lds[2 * kBlock + p], acm[2 * kBlock]);
+                active = false;
+            }
+        }
+    }
+    store_sums<PTMI_MESH_PLANES != 0>(work_item<(FL & F_TLIST) != 0>(S0, WP, item, lane), WP, sums, part, acc_lds[0 * kBlock + tid],
+                                      acc_lds[1 * kBlock + tid], acc_lds[2 * kBlock + tid]);
+}
+
 // Per-item duration onto its tile's cost accumulator (WorkPlan::cost, tile_order_kernel;
 // mesh kernels only).  Off in the product (PTMI_TILE_COST 0): the clock read at an item's
 // start (s_memrealtime, an intrinsic with side effects) made the uniform-load analysis treat
@@ -2548,7 +2723,10 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
 #if PTMI_TILE_COST
         const unsigned long long c0 = WP.cost ? wall_clock64() : 0ull;
 #endif
-        trace_groups<FL>(S, samples, WP, seeds, sunf, sums, part, item);
+        if constexpr (kPoolOf<FL>)
+            trace_groups_pool<FL>(S, samples, WP, seeds, sunf, sums, part, item);
+        else
+            trace_groups<FL>(S, samples, WP, seeds, sunf, sums, part, item);
 #if PTMI_TILE_COST
         item_cost_add(S, WP, item, c0);
 #endif

@@ -90,8 +90,10 @@ def test_full_frame_matches_live_reference(cfg, scene, ap, fl):
 def test_eight_gpu_shards_sum_to_frame_at_full_resolution(scene, ap, fl, split):
     """The shards 8 ranks render (C3: cost-balanced sample ranges; C5: 8x8 tiles, owned
     diagonally -- 160 tiles per row divide by 8, ptmi_api.cpp render) summed in rank order
-    equal the one-GPU frame: bit-identical for the tile split, FP64 summation order for the
-    sample split."""
+    equal the one-GPU frame: bit-identical for the tile split (at S = 48 every tile is one
+    item in both plans, and the mesh kernels' path pool runs an item the same way whatever
+    the launch's tile list), FP64 summation order for the sample split.  A tile-split share
+    rendered twice is bit-identical too (the pool is deterministic)."""
     import torch
     W, H, S, world = 1280, 960, 48, 8
     objs, tris, grps, cam = scene_inputs(scene, W, H, ap, fl)
@@ -113,6 +115,14 @@ def test_eight_gpu_shards_sum_to_frame_at_full_resolution(scene, ap, fl, split):
         assert torch.equal(acc, full)
     else:
         assert (acc - full).abs().max().item() < 1e-12 * S
+    if split == "tile":
+        sc = api.Scene(0, objs, tris, grps, cam)
+        s0, s1, ts, to = pdist.shard(world - 1, world, S, split)
+        again = torch.empty_like(full)
+        sc.render(S, s0, s1, seeds.data_ptr(), again.data_ptr(), tile_stride=ts, tile_offset=to)
+        torch.cuda.synchronize()
+        sc.close()
+        assert torch.equal(again, part)
 
 
 @pytest.mark.parametrize("scene,split", [("reference", "tile"), ("gopher", "tile"), ("reference", "sample")])

@@ -56,7 +56,8 @@ def test_measured_order_never_changes_the_sums(scene):
         pytest.fail("libptmi_study.so not built (make -C pathtracer-ocl_amd study)")
     study = api.load_library(api.STUDY_LIB_PATH)
     w, h, spp = 320, 240, 48
-    raster = _renders(0, scene, w, h, spp, 1, 3, 1, chunks=4)[0]
+    # (the study library is built without the product's path pool: its raster launch is the reference)
+    raster = _renders(0, scene, w, h, spp, 1, 3, 1, chunks=4, lib=study)[0]
     measured = _renders(2, scene, w, h, spp, 3, 3, 1, chunks=4, lib=study)
     for m in measured:  # launch 1: static order; launches 2, 3: orders from measured costs
         assert np.array_equal(raster, m)
