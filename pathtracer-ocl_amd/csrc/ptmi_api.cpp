@@ -90,6 +90,7 @@ struct ptmi_scene {
     uint32_t mesh_items_share = 48;  // ... in a sample-split rank's share (a sub-range of the samples)
     uint32_t min_chunk = 32;   // fewest samples per chunk item (see render)
     uint32_t tail_split = 4;   // mesh scenes: the last chunk round cut into this many (see render)
+    uint32_t tail_min = 0;     // ... while those keep at least this many samples; 0: automatic (see render)
     // Mesh scenes: per-tile cost class (mesh_tile_cost) and the dispatch order built from it
     // for the last (tile_stride, tile_offset) rendered (see render).
     // 0: raster order, 1: static (hull-hit classes), 2: measured by the last launch (needs a
@@ -500,6 +501,14 @@ hipError_t resident_waves(ptmi_scene* s) {
 // heuristic, not an exactness argument.
 constexpr uint8_t kCostUnset = 0xFF;
 
+// The mesh kernels' walk batch for a scene (DevScene::walk_batch): larger meshes have longer walks
+// (gopher: 9.8 Node4 visits and 5.3 triangle tests per walk against the teapot's 6.7 and 2.3), so
+// a walk phase is worth more parked lanes.  Scenes without meshes never walk.
+static int32_t walk_batch_for(const HostScene& hs) {
+    if (!(hs.flags & 1)) return 64;
+    return hs.n_tri >= 12000 ? 32 : 28;
+}
+
 TileCostInput tile_cost_input(const HostScene& hs) {
     TileCostInput in;
     in.cam = hs.cam;
@@ -661,6 +670,12 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     s->dev.n_nodes = hs.n_grp;
     s->dev.n_nodes4 = (int32_t)hs.index.nodes.size();
     s->dev.leaf_bit = hs.leaf_bit;
+    // Walk batch of the mesh kernels (parked lanes that start a wave's walk phase; ptmi_kernels.hip
+    // trace_groups / trace_groups_pool): a walk phase lasts as long as its longest walk, so the
+    // batch trades the parked lanes' waiting against the phases' idle lanes.  Round 6, with the
+    // path pool (2048 spp, one MI355X, profiles/r6/tune): teapot (C4) 24 / 28 / 32 -> 490.5 / 489.4 /
+    // 493.6 ms, gopher (C5) 784.2 / 768.2 / 759.6 ms.
+    s->dev.walk_batch = walk_batch_for(hs);
     // (Tests and tuning studies change the plan through ptmi_diag_set_knob; the library reads
     // no tuning variable from the environment.)
     // Mesh scenes: >= 64 samples per chunk.  It binds only on short sample ranges (a rank's
@@ -1017,9 +1032,14 @@ int ptmi_scene_render(ptmi_scene* s, uint32_t samples, uint32_t sample_begin, ui
     // while the short chunks keep >= min_chunk / 2 samples: on 8-rank shares (64-sample chunks)
     // 16-sample ones cost C4's sample split more at each item's end than they saved at the
     // launch's (projected efficiency 0.893 -> 0.878) and left C5's tile split as it was.
-    // Chunks are summed in chunk order either way.
+    // Round 6: the path-pool kernels (affine mesh scenes in parity mode) have no per-item lane
+    // drain, so their short chunks may go down to 8 samples (tail_min): an 8-rank C5 tile share
+    // (38-sample chunks) drained 9.8 ms of its 108.9 ms on its last round's costliest tiles
+    // (profiles/r6/timeline).  Chunks are summed in chunk order either way.
+    const bool pooled = (kflags0 & 1) && !(kflags0 & (16 | 32 | 64));  // F_GROUPS, not F_PROJ / F_TEX / F_XRNG
+    const uint32_t tail_min = s->tail_min ? s->tail_min : pooled ? 8u : s->min_chunk / 2;
     const uint32_t tl = (chunk_len + std::max<uint32_t>(s->tail_split, 1) - 1) / std::max<uint32_t>(s->tail_split, 1);
-    if (!split && auto_chunks && (s->flags & 1) && chunks > 1 && s->tail_split > 1 && tl >= s->min_chunk / 2) {
+    if (!split && auto_chunks && (s->flags & 1) && chunks > 1 && s->tail_split > 1 && tl >= tail_min) {
         const uint32_t rest = range - (chunks - 1) * chunk_len;
         wp.n_long = chunks - 1;
         wp.tail_len = tl;
@@ -1609,6 +1629,8 @@ extern "C" int ptmi_diag_set_knob(ptmi_scene* s, int knob, int value) {
     case PTMI_KNOB_MESH_ITEMS_SHARE: s->mesh_items_share = pos; return PTMI_OK;
     case PTMI_KNOB_MIN_CHUNK: s->min_chunk = pos; return PTMI_OK;
     case PTMI_KNOB_TAIL_SPLIT: s->tail_split = pos; return PTMI_OK;
+    case PTMI_KNOB_TAIL_MIN: s->tail_min = (uint32_t)std::max(0, value); return PTMI_OK;
+    case PTMI_KNOB_WALK_BATCH: s->dev.walk_batch = (int32_t)std::min<uint32_t>(pos, 64); return PTMI_OK;
     case PTMI_KNOB_TILE_ORDER:
         // 2 (the order measured by the last launch) needs the item timing that only the study
         // build compiles in (ptmi_kernels.hip PTMI_TILE_COST).

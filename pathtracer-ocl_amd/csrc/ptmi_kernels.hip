@@ -157,10 +157,8 @@ static constexpr double kPi = (double)3.14159265359f;  // tracer.cl:1 (a float l
 #define PTMI_REFILL_STARVE_GROUPS 12
 #endif
 static constexpr int kRefillNeed = PTMI_REFILL_NEED;
-#ifndef PTMI_WALK_BATCH
-#define PTMI_WALK_BATCH 24
-#endif
-static constexpr int kWalkBatch = PTMI_WALK_BATCH;  // parked lanes that trigger a wave's BVH walk phase
+// The walk batch -- parked lanes that start a wave's BVH walk phase -- is a scene value since round 6
+// (DevScene::walk_batch, chosen in ptmi_api.cpp).
 
 struct d4 {
     double x, y, z, w;
@@ -2270,13 +2268,13 @@ __device__ __forceinline__ const DevScene& scene_reload(const DevScene& S) {
 // trace_kernel's body for scenes with BVH groups: the loop of the other scenes, with
 // the BVH walks deferred.  A lane whose ray needs a walk (group_needs_walk) parks
 // (pending, keeping its primitives' best in LDS) and the wave walks all parked lanes
-// together once kWalkBatch are parked or no lane is ready to shade -- a walk costs the
+// together once S.walk_batch are parked or no lane is ready to shade -- a walk costs the
 // whole wave its longest traversal, so it should run with many lanes, not the ~10 % of
 // rays that reach a mesh in any one bounce.  Each lane still traces its samples in
 // order, and the closest hit does not depend on when or in which order candidates are
 // examined (lexicographic minimum, better()).
-// Path pool (round 6; every affine narrow-code mesh kernel, i.e. trace_kernel<1|3|5|...> and the
-// F_TLIST ones).  A mesh work item is one tile's chunk of samples, lane t tracing pixel t's samples
+// Path pool (round 6; every affine mesh kernel: trace_kernel<1|3|5|...>, the F_TLIST and the F_WIDE
+// ones).  A mesh work item is one tile's chunk of samples, lane t tracing pixel t's samples
 // in order, so a lane that has traced its chunk idled until the wave's slowest lane was done: 5.7 %
 // of the one-GPU loop lane-cycles and 12-15 % of an 8-rank tile share's, whose chunks are short
 // (C5 at N = 8: 55 chunks of 38 samples; profiles/r5/timeline).  With the pool a wave's lanes take
@@ -2292,13 +2290,13 @@ __device__ __forceinline__ const DevScene& scene_reload(const DevScene& S) {
 // LDS stays at 16 waves per CU (10,112 B per wave); spill 48 -> 16 B/lane (trace_kernel<5>).
 // 2048 spp, one MI355X, same box (profiles/r6/pool): C4 528.3 -> 489.8 ms, C5 822.9 -> 784.3 ms;
 // 8-rank shares (tools/shard_balance.py): C5 tile split Sigma/T1 1.195 -> 1.050, projected
-// efficiency 0.831 -> 0.941.  (The generic, wide-code and statistical-RNG mesh kernels keep
-// trace_groups; PTMI_POOL=0 builds the diagnostic libraries without the pool.)
+// efficiency 0.831 -> 0.941.  (The generic and statistical-RNG mesh kernels keep trace_groups;
+// PTMI_POOL=0 builds the diagnostic libraries without the pool.)
 #ifndef PTMI_POOL
 #define PTMI_POOL 1
 #endif
 template <int FL>
-constexpr bool kPoolOf = PTMI_POOL != 0 && (FL & F_GROUPS) != 0 && !(FL & (F_PROJ | F_WIDE | F_XRNG));
+constexpr bool kPoolOf = PTMI_POOL != 0 && (FL & F_GROUPS) != 0 && !(FL & (F_PROJ | F_XRNG));
 template <int FL>
 __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t samples, const WorkPlan& WP,
                                              const double* __restrict__ seeds, const double* __restrict__ sunf,
@@ -2452,7 +2450,7 @@ __device__ __forceinline__ void trace_groups(const DevScene& S0, uint32_t sample
         PTMI_TADD(13, t_b);
         PTMI_TSTAMP(t_c);
         const int n_pend = __popcll(__ballot(pending));
-        if (n_pend >= kWalkBatch || (n_pend > 0 && !__any(ready))) {
+        if (n_pend >= S.walk_batch || (n_pend > 0 && !__any(ready))) {
             PTMI_WADD(8, 1ull);
             PTMI_WADD(9, (unsigned long long)n_pend);
             if (pending) {
@@ -2521,7 +2519,7 @@ __device__ __forceinline__ void trace_groups_pool(const DevScene& S0, uint32_t s
     constexpr int kCamComp = kDof ? 6 : 3;
     constexpr int kPoolStack = 21;  // ptmi_bvh.cpp kMaxNode4Depth * 3
     static_assert(kPoolStack <= kStack, "pool stack");
-    __shared__ StackEntry<true> stk_lds[kPoolStack * kStkStride];
+    __shared__ StackEntry<!(FL & F_WIDE)> stk_lds[kPoolStack * kStkStride];  // 32-bit codes: F_WIDE
     __shared__ double acc_lds[3 * kBlock];  // colour sum of pixel t of the tile at [k * 64 + t]
     __shared__ double acm_lds[3 * kBlock];  // accumColor / mask of the lane's path (as trace_groups)
     __shared__ double msk_lds[3 * kBlock];
@@ -2635,7 +2633,7 @@ __device__ __forceinline__ void trace_groups_pool(const DevScene& S0, uint32_t s
             }
         }
         const int n_pend = __popcll(__ballot(pending));
-        if (n_pend >= kWalkBatch || (n_pend > 0 && !__any(ready))) {
+        if (n_pend >= S.walk_batch || (n_pend > 0 && !__any(ready))) {
             if (pending) {
                 h = Hit{hp_t_lds[tid], hp_pk_lds[tid], -1, -1, 0.0, 0.0};
                 group_walks<A>(S, stk, P.ro, P.rd, h);
@@ -2658,6 +2656,132 @@ __device__ __forceinline__ void trace_groups_pool(const DevScene& S0, uint32_t s
     }
     store_sums<PTMI_MESH_PLANES != 0>(work_item<(FL & F_TLIST) != 0>(S0, WP, item, lane), WP, sums, part, acc_lds[0 * kBlock + tid],
                                       acc_lds[1 * kBlock + tid], acc_lds[2 * kBlock + tid]);
+}
+
+// The path pool for the kernels without meshes (PTMI_POOL_FLAT, affine non-DoF parity-mode scenes):
+// the loop of trace_kernel's else branch with trace_groups_pool's path hand-out.  Measured and off:
+// their items are mostly whole tiles (2048 samples per lane, no per-item drain to remove), and what
+// the pool saves in registers (C2: 69 instead of 72 VGPRs at 7 waves, or 8 waves at 64 VGPRs with
+// 16 B/lane of spill, 5,120 B of LDS) does not pay for its LDS reads and atomics: 2048 spp, same
+// box, C2 144.46 ms -> 146.9 (7 waves) / 145.3 ms (8 waves) (profiles/r6/tune/ab2).
+#ifndef PTMI_POOL_FLAT
+#define PTMI_POOL_FLAT 0
+#endif
+#ifndef PTMI_POOL_FGI2_SEED
+#define PTMI_POOL_FGI2_SEED 1  // fgi2 recomputed from the seed at the camera refill (no LDS table)
+#endif
+template <int FL>
+constexpr bool kPoolFlatOf = PTMI_POOL_FLAT != 0 && !(FL & (F_GROUPS | F_PROJ | F_XRNG | F_TEX | F_DOF));
+template <int FL>
+__device__ __forceinline__ void trace_flat_pool(const DevScene& S0, uint32_t samples, const WorkPlan& WP,
+                                                const double* __restrict__ seeds, const double* __restrict__ sunf,
+                                                double* __restrict__ sums, double* __restrict__ part) {
+    constexpr bool A = true;
+    constexpr bool kDof = (FL & F_DOF) != 0;
+    constexpr int kCamComp = kDof ? 6 : 3;
+    __shared__ double acc_lds[3 * kBlock];
+    __shared__ double acm_lds[3 * kBlock];
+    __shared__ double cam_lds[kCamComp * kBlock];
+    __shared__ uint32_t ncur_lds[kBlock];
+    __shared__ float fgi_lds[kBlock];
+    __shared__ float fgi2_lds[PTMI_POOL_FGI2_SEED ? 1 : kBlock];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const Item it = work_item(S0, WP, blockIdx.x, lane);
+    if (!it.ok) return;
+    {
+        const double seed0 = it.inside ? seeds[it.i] : 0.0;
+        fgi_lds[tid] = (float)(seed0 / (double)S0.n_list);
+        if (!PTMI_POOL_FGI2_SEED) fgi2_lds[tid] = (float)(seed0 / (double)samples);
+    }
+    const int W = S0.cam.width, H = S0.cam.height;
+    acc_lds[0 * kBlock + tid] = 0.0;
+    acc_lds[1 * kBlock + tid] = 0.0;
+    acc_lds[2 * kBlock + tid] = 0.0;
+    const int tx0 = __builtin_amdgcn_readfirstlane(it.px - (lane & 7));
+    const int ty0 = __builtin_amdgcn_readfirstlane(it.py - (lane >> 3));
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)it.c0);
+    const uint32_t total = 64u * ((uint32_t)__builtin_amdgcn_readfirstlane((int)it.c1) - c0);
+    double* acm = acm_lds + tid;
+    uint32_t j_next = 0, buf_id = 0;
+    bool buffered = false, active = false;
+    PathState P;
+    for (;;) {
+        if (!__any(active || buffered) && j_next >= total) break;
+        const DevScene& S = scene_reload<(PTMI_SCENE_RELOAD & 2) != 0>(S0);
+        const uint32_t avail = total - j_next;
+        const uint64_t m_idle = __ballot(!buffered && !active), m_busy = __ballot(!buffered && active);
+        const uint32_t n_idle = min((uint32_t)__popcll(m_idle), avail);
+        const uint32_t n_need = min((uint32_t)(__popcll(m_idle) + __popcll(m_busy)), avail);
+        if (n_need >= (uint32_t)kRefillNeed || n_idle >= (uint32_t)PTMI_REFILL_STARVE || (n_idle > 0 && !__any(active))) {
+            const uint32_t rank = active ? (uint32_t)__popcll(m_idle) + __builtin_amdgcn_mbcnt_hi(
+                                                                            (uint32_t)(m_busy >> 32),
+                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m_busy, 0u))
+                                         : __builtin_amdgcn_mbcnt_hi((uint32_t)(m_idle >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m_idle, 0u));
+            if (!buffered && rank < avail) {
+                const uint32_t j = j_next + rank;
+                const uint32_t p = j & 63u, n = c0 + (j >> 6);
+                const int px = tx0 + (int)(p & 7u), py = ty0 + (int)(p >> 3);
+                float fgi2;
+                if (PTMI_POOL_FGI2_SEED) {
+                    const double sd = (px < W && py < H) ? seeds[(uint32_t)py * (uint32_t)W + (uint32_t)px] : 0.0;
+                    fgi2 = (float)(sd / (double)samples);
+                } else {
+                    fgi2 = fgi2_lds[p];
+                }
+                const DevCamera& cam = camera_ptr<(PTMI_CAM_RELOAD & 1) != 0>(S);
+                d4 ro, rd;
+                float rx, ry;
+                camera_offsets<FL>(fgi_lds[p], fgi2, XSeed{}, n, rx, ry);
+                ray_for_pixel<kDof, A>(cam, sunf, (unsigned)px, (unsigned)py, rx, ry, (int)n, ro, rd);
+                double* cb = cam_lds + tid;
+                cb[0 * kBlock] = rd.x;
+                cb[1 * kBlock] = rd.y;
+                cb[2 * kBlock] = rd.z;
+                if constexpr (kCamComp > 3) {
+                    cb[3 * kBlock] = ro.x;
+                    cb[4 * kBlock] = ro.y;
+                    cb[5 * kBlock] = ro.z;
+                }
+                buf_id = j;
+                buffered = true;
+            }
+            j_next += n_need;
+        }
+        if (!active && buffered) {
+            const double* cb = cam_lds + tid;
+            const d4 crd = mk(cb[0 * kBlock], cb[1 * kBlock], cb[2 * kBlock], 0.0);
+            d4 cro;
+            if constexpr (kCamComp > 3) {
+                cro = mk(cb[3 * kBlock], cb[4 * kBlock], cb[5 * kBlock], 1.0);
+            } else {
+                const double* co = camera_ptr<(PTMI_CAM_RELOAD & 1) != 0>(S).origin;
+                cro = mk(co[0], co[1], co[2], 1.0);
+            }
+            start_path<A, kDof>(P, cro, crd);
+            acm[0 * kBlock] = 0.0;
+            acm[1 * kBlock] = 0.0;
+            acm[2 * kBlock] = 0.0;
+            ncur_lds[tid] = buf_id;
+            buffered = false;
+            active = true;
+        }
+        if (active) {
+            Hit h;
+            if (P.dead) h.pk = -1;
+            else h = find_closest_prims<FL>(S, P.ro, P.rd);
+            const uint32_t id = ncur_lds[tid];
+            if (bounce_shade<FL, true>(S, P, h, fgi_lds[id & 63u], c0 + (id >> 6), acm)) {
+                const uint32_t p = id & 63u;
+                atomicAdd(&acc_lds[0 * kBlock + p], acm[0 * kBlock]);
+                atomicAdd(&acc_lds[1 * kBlock + p], acm[1 * kBlock]);
+                atomicAdd(&acc_lds[2 * kBlock + p], acm[2 * kBlock]);
+                active = false;
+            }
+        }
+    }
+    store_sums<true>(work_item(S0, WP, blockIdx.x, lane), WP, sums, part, acc_lds[0 * kBlock + tid],
+                     acc_lds[1 * kBlock + tid], acc_lds[2 * kBlock + tid]);
 }
 
 // Per-item duration onto its tile's cost accumulator (WorkPlan::cost, tile_order_kernel;
@@ -2736,6 +2860,8 @@ __global__ __launch_bounds__(kBlock, (FL & F_GROUPS)      ? PTMI_WAVES_GROUPS
             ptmi_tl[2 * item + 1] = wall_clock64();
         }
 #endif
+    } else if constexpr (kPoolFlatOf<FL>) {
+        trace_flat_pool<FL>(S, samples, WP, seeds, sunf, sums, part);
     } else {
         constexpr bool A = !(FL & F_PROJ);
         const int tid = threadIdx.x, lane = tid & 63;

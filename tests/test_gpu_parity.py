@@ -369,8 +369,9 @@ def _assert_ref_defined(objs, t2, g2, cam, spp, seeds):
 def test_hip_matches_live_reference_wide_child_codes():
     """A mesh past 16-bit child codes (tests/adversarial.py "big", 34,848 triangles) takes
     the wide codes and the affine F_WIDE instantiation's 32-bit traversal stack (round 6; it
-    had been sent to the generic instantiation): still the reference's image, and the generic
-    instantiation's bit for bit."""
+    had been sent to the generic instantiation; it takes the path pool too): still the
+    reference's image, and every path the generic instantiation's bit for bit (_paths; the
+    frames differ only in the pool's summation order)."""
     if not pyoracle.ref_available():
         pytest.skip("oracle/_ref not built")
     from tests import adversarial
@@ -390,7 +391,8 @@ def test_hip_matches_live_reference_wide_child_codes():
     assert err < 1e-12, "big: L-inf %.3e vs live reference" % err
     with api.force_flags(31):  # the generic instantiation (literal double4 arithmetic)
         gen = api.Trace(objs, tris, grps, 0, spp, cam, seeds=seeds)
-    assert np.array_equal(out, gen)
+    assert np.abs(out - gen).max() < 1e-15
+    assert np.array_equal(_paths(objs, tris, grps, cam, spp, seeds), _paths(objs, tris, grps, cam, spp, seeds, 31))
 
 
 def test_wide_code_scene_statistical_rng():

@@ -40,4 +40,4 @@ base = None
 for name, (ms, fl, img) in res.items():
     print("%-38s flags %3d  %8.2f ms per %dx%d x %d spp frame" % (name, fl, ms, W, H, S))
 a, b = [v[2] for v in res.values()]
-print("images bit-identical:", bool(torch.equal(a, b)))
+print("images bit-identical:", bool(torch.equal(a, b)), " max |diff| of the sums: %.3e" % (a - b).abs().max().item())
