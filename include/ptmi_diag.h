@@ -59,7 +59,8 @@ int ptmi_diag_split_passes(const ptmi_scene* s);
  * (study build only); TAIL_SPLIT: a mesh scene's automatic plan cuts its last chunk round into
  * this many shorter rounds (1 = off); TAIL_MIN: the fewest samples of such a short chunk (0 =
  * automatic: 8 for the path-pool kernels, MIN_CHUNK / 2 otherwise); WALK_BATCH: parked lanes that
- * start a mesh kernel's walk phase (1-64; default by scene, ptmi_api.cpp).  PTMI_ERR_UNSUPPORTED for a knob or value this build
+ * start a mesh kernel's walk phase (1-64; default by scene, ptmi_api.cpp); HEMI_MESH: 1 = the mesh
+ * kernels read the hemisphere table, 0 = they compute it (default by index size).  PTMI_ERR_UNSUPPORTED for a knob or value this build
  * lacks. */
 enum {
     PTMI_KNOB_TAIL_TILES = 1,
@@ -74,7 +75,8 @@ enum {
     PTMI_KNOB_TAIL_SPLIT = 10,
     PTMI_KNOB_MESH_ITEMS_SHARE = 11,
     PTMI_KNOB_TAIL_MIN = 12,
-    PTMI_KNOB_WALK_BATCH = 13
+    PTMI_KNOB_WALK_BATCH = 13,
+    PTMI_KNOB_HEMI_MESH = 14
 };
 int ptmi_diag_set_knob(ptmi_scene* s, int knob, int value);
 

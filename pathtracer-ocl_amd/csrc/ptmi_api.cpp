@@ -504,6 +504,13 @@ constexpr uint8_t kCostUnset = 0xFF;
 // The mesh kernels' walk batch for a scene (DevScene::walk_batch): larger meshes have longer walks
 // (gopher: 9.8 Node4 visits and 5.3 triangle tests per walk against the teapot's 6.7 and 2.3), so
 // a walk phase is worth more parked lanes.  Scenes without meshes never walk.
+// Bytes of a scene's traversal index as the mesh kernels read it: Node4s, the triangles' DevTri
+// and DevTriShade records and their gate-chain boxes (teapot ~1.4 MB, gopher ~3.7 MB).
+static size_t index_bytes(const HostScene& hs) {
+    return hs.index.nodes.size() * sizeof(Node4) + hs.index.tris.size() * sizeof(DevTri) +
+           hs.st.size() * sizeof(DevTriShade) + hs.index.chain_boxes.size() * sizeof(ChainBox);
+}
+
 static int32_t walk_batch_for(const HostScene& hs) {
     if (!(hs.flags & 1)) return 64;
     return hs.n_tri >= 12000 ? 32 : 28;
@@ -676,6 +683,12 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     // path pool (2048 spp, one MI355X, profiles/r6/tune): teapot (C4) 24 / 28 / 32 -> 490.5 / 489.4 /
     // 493.6 ms, gopher (C5) 784.2 / 768.2 / 759.6 ms.
     s->dev.walk_batch = walk_batch_for(hs);
+    // The hemisphere table in the mesh kernels: the 1-MB (sin, cos) plane shares each XCD's 4-MB L2
+    // with the traversal index.  Round 6, with the path pool, C5 (gopher, index ~3.7 MB) renders in the
+    // same time without it (766.5 / 764.7 against 766.0 / 765.4 ms) and its HBM traffic falls from
+    // 2.25 to 0.76 GB per launch (profiles/r6/hbm1): the table's lines were being evicted and
+    // refetched.  Smaller indexes keep it (before the pool C4 was 2.8 % slower without it).
+    s->dev.hemi_mesh = index_bytes(hs) <= (2u << 20) ? 1 : 0;
     // (Tests and tuning studies change the plan through ptmi_diag_set_knob; the library reads
     // no tuning variable from the environment.)
     // Mesh scenes: >= 64 samples per chunk.  It binds only on short sample ranges (a rank's
@@ -1631,6 +1644,7 @@ extern "C" int ptmi_diag_set_knob(ptmi_scene* s, int knob, int value) {
     case PTMI_KNOB_TAIL_SPLIT: s->tail_split = pos; return PTMI_OK;
     case PTMI_KNOB_TAIL_MIN: s->tail_min = (uint32_t)std::max(0, value); return PTMI_OK;
     case PTMI_KNOB_WALK_BATCH: s->dev.walk_batch = (int32_t)std::min<uint32_t>(pos, 64); return PTMI_OK;
+    case PTMI_KNOB_HEMI_MESH: s->dev.hemi_mesh = value != 0; return PTMI_OK;
     case PTMI_KNOB_TILE_ORDER:
         // 2 (the order measured by the last launch) needs the item timing that only the study
         // build compiles in (ptmi_kernels.hip PTMI_TILE_COST).

@@ -169,6 +169,7 @@ struct DevScene {
     const DevTriShade* tri_shade;
     int32_t leaf_bit;  // kLeafNarrow or kLeafWide (Node4 child codes)
     int32_t walk_batch;  // parked lanes that start a wave's BVH walk phase (mesh kernels; ptmi_api.cpp)
+    int32_t hemi_mesh;   // mesh kernels read the hemisphere table's (sin, cos) plane (1) or compute (0)
     uint32_t n_obj;   // intersectable objects in objs[]
     uint32_t n_nodes, n_tri;
     uint32_t n_list;  // numObjects of the reference's list (fgi = seed / numObjects, tracer.cl:840)

@@ -1623,7 +1623,8 @@ __device__ __forceinline__ void hemi_sqrt(float u2, double& r2s, double& rc) {
 #ifndef PTMI_HEMI_TAB_GROUPS
 #define PTMI_HEMI_TAB_GROUPS 1  // mesh scenes read the table too (round 5: with the group kernel's colour
                                 // state in LDS, 2048 spp: C4 594 -> 577, C5 902 -> 897 ms; in round 4 the
-                                // 2 MB table's L2 share had cost C5 ~1.5 % at 512 spp)
+                                // 2 MB table's L2 share had cost C5 ~1.5 % at 512 spp) -- since round 6 only
+                                // where the scene allows it (DevScene::hemi_mesh, ptmi_api.cpp)
 #endif
 static constexpr int kHemiBits = 16;
 static constexpr int kHemiSize = 1 << kHemiBits;
@@ -1644,10 +1645,12 @@ __device__ __forceinline__ int hemi_slot(float u) {  // table record of u, or -1
 #ifndef PTMI_HEMI_SQRT_GROUPS
 #define PTMI_HEMI_SQRT_GROUPS 0  // mesh kernels read the sqrt plane too (1) or compute the pair (0)
 #endif
+// `use` (uniform): the scene lets this kernel read the table (DevScene::hemi_mesh for the mesh kernels).
 template <bool A, bool kTab, bool kTabSqrt = kTab>
-__device__ __forceinline__ d4 random_hemisphere(const double* __restrict__ tab, d4 nv, float u1, float u2) {
+__device__ __forceinline__ d4 random_hemisphere(const double* __restrict__ tab, d4 nv, float u1, float u2,
+                                                bool use = true) {
     double sr, cr, rand2s, rc;
-    const int k1 = kTab ? hemi_slot(u1) : -1;
+    const int k1 = (kTab && use) ? hemi_slot(u1) : -1;
     if (k1 >= 0) {
         const double2 q = *reinterpret_cast<const double2*>(tab + 2 * k1);
         sr = q.x;
@@ -1656,7 +1659,7 @@ __device__ __forceinline__ d4 random_hemisphere(const double* __restrict__ tab, 
         PTMI_WADD(35, 1ull);
         hemi_sincos<A>(u1, sr, cr);
     }
-    const int k2 = kTabSqrt ? hemi_slot(u2) : -1;
+    const int k2 = (kTabSqrt && use) ? hemi_slot(u2) : -1;
     if (k2 >= 0) {
         const double2 q = *reinterpret_cast<const double2*>(tab + 2 * kHemiSize + 2 * k2);
         rand2s = q.x;
@@ -2040,7 +2043,8 @@ __device__ __forceinline__ bool bounce_shade(const DevScene& S, PathState& P, co
         // Only affine instantiations read the table: its records are the affine sequences'
         // results, so they equal what such a lane computes by construction.
         P.rd = random_hemisphere<A, A && (PTMI_HEMI_TAB_GROUPS || !(FL & F_GROUPS)),
-                                 A && (PTMI_HEMI_SQRT_GROUPS || !(FL & F_GROUPS))>(S.hemi, nv, u1, u2);
+                                 A && (PTMI_HEMI_SQRT_GROUPS || !(FL & F_GROUPS))>(S.hemi, nv, u1, u2,
+                                                                                 !(FL & F_GROUPS) || S.hemi_mesh);
         cosine = dotv<A>(P.rd, nv);
     }
     P.ro = over;

@@ -31,7 +31,7 @@ RNG_NOISE3D, RNG_XOSHIRO = 0, 1  # ptmi_scene_set_rng: parity (default) / opt-in
 # ptmi_diag_set_knob (include/ptmi_diag.h): work-plan knobs of a resident scene
 (KNOB_TAIL_TILES, KNOB_TAIL_ITEMS, KNOB_MESH_ITEMS, KNOB_MIN_CHUNK, KNOB_TILE_ORDER, KNOB_SPLIT_CHUNK,
  KNOB_SPLIT_SLOTS, KNOB_SPLIT_SYNC, KNOB_SPLIT_BUDGET, KNOB_TAIL_SPLIT, KNOB_MESH_ITEMS_SHARE, KNOB_TAIL_MIN,
- KNOB_WALK_BATCH) = range(1, 14)
+ KNOB_WALK_BATCH, KNOB_HEMI_MESH) = range(1, 15)
 
 EXPORTS = ("ptmi_trace", "ptmi_device_count", "ptmi_device_name", "ptmi_scene_create", "ptmi_scene_destroy",
            "ptmi_scene_size", "ptmi_scene_render", "ptmi_finalize", "ptmi_fill_seeds", "ptmi_build_info",

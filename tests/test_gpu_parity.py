@@ -275,6 +275,25 @@ def test_whole_tiles_and_chunked_tail(scene, stride):
     assert torch.all(torch.isfinite(acc))
 
 
+@pytest.mark.parametrize("scene", ["teapot", "gopher"])
+def test_mesh_hemisphere_table_switch(scene):
+    """The mesh kernels read the hemisphere table only where the scene's index leaves it room in
+    L2 (DevScene::hemi_mesh, ptmi_api.cpp: the teapot yes, the gopher no).  The table holds the
+    bits the kernel computes, so either way the frame is the same, bit for bit."""
+    torch, sc = _torch_scene(scene, 64, 48)
+    S, n = 40, 64 * 48
+    seeds = torch.tensor(layout.seeds_go_float64(n, 21), dtype=torch.float64, device="cuda")
+    frames = []
+    for v in (0, 1):
+        assert sc.set_knob(api.KNOB_HEMI_MESH, v) == api.PTMI_OK
+        f = torch.empty(n * 4, dtype=torch.float64, device="cuda")
+        sc.render(S, 0, S, seeds.data_ptr(), f.data_ptr())
+        frames.append(f)
+    torch.cuda.synchronize()
+    sc.close()
+    assert torch.equal(frames[0], frames[1])
+
+
 def test_tile_split_partitions_frame():
     torch, sc = _torch_scene("teapot", 40, 24)
     S, n = 3, 40 * 24
