@@ -171,8 +171,13 @@ int ptmi_scene_size(const ptmi_scene* s, uint32_t* width, uint32_t* height);
  *   chunks     : sample chunks per pixel for every owned tile (load balance), or
  *                0 = auto: most tiles are one work item over the whole range
  *                (summed in sample order), the tiles at the end of the launch are
- *                split into chunks.  Chunk sums are combined in a fixed order, so
- *                results are deterministic.
+ *                split into chunks; mesh scenes chunk every tile.  Chunk sums are
+ *                combined in a fixed order, so results are deterministic.  The
+ *                affine mesh kernels hand a work item's (pixel, sample) paths to
+ *                whichever lanes are free (the path pool) and add a pixel's paths
+ *                in completion order: every path is the reference's, the sums
+ *                differ from sample order only by FP64 rounding, and a render
+ *                is reproducible bit for bit.
  * Sample indices are GLOBAL (fgi2 = seed/samples and the DoF aperture pattern
  * depend on n and on the total, tracer.cl:841, 766), so any split of
  * [0, samples) sums to the same frame.
@@ -217,8 +222,8 @@ const char* ptmi_build_info(void);
  *   them  [4] largest root scale exponent s (bounds stored as (b - ctr) / 2^s)
  *   [5] roots  [6] longest chain of Node4s (the walk's stack holds <= 3 entries per
  *   level; ptmi_bvh.cpp keeps it <= 7)  [7] the child codes' leaf bit: 2^15 when every
- *   code fits the affine kernels' 16-bit traversal stack, else 2^30 (the scene then runs
- *   the generic instantiation, 32-bit stack).  Index quality (box inflation from the
+ *   code fits the affine kernels' 16-bit traversal stack, else 2^30 (an affine scene then
+ *   runs the wide-code instantiation, 32-bit stack).  Index quality (box inflation from the
  *   binary16 bounds) can be compared across translated or scaled copies of one mesh. */
 int ptmi_index_stats(const void* objects, uint32_t n_obj, const void* triangles, uint32_t n_tri,
                      const void* groups, uint32_t n_grp, const void* camera, double* out, int n_out,

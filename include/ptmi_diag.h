@@ -60,7 +60,7 @@ int ptmi_diag_split_passes(const ptmi_scene* s);
  * this many shorter rounds (1 = off); TAIL_MIN: the fewest samples of such a short chunk (0 =
  * automatic: 8 for the path-pool kernels, MIN_CHUNK / 2 otherwise); WALK_BATCH: parked lanes that
  * start a mesh kernel's walk phase (1-64; default by scene, ptmi_api.cpp); HEMI_MESH: 1 = the mesh
- * kernels read the hemisphere table, 0 = they compute it (default by index size).  PTMI_ERR_UNSUPPORTED for a knob or value this build
+ * kernels read the hemisphere table (default), 0 = they compute it.  PTMI_ERR_UNSUPPORTED for a knob or value this build
  * lacks. */
 enum {
     PTMI_KNOB_TAIL_TILES = 1,

@@ -504,13 +504,6 @@ constexpr uint8_t kCostUnset = 0xFF;
 // The mesh kernels' walk batch for a scene (DevScene::walk_batch): larger meshes have longer walks
 // (gopher: 9.8 Node4 visits and 5.3 triangle tests per walk against the teapot's 6.7 and 2.3), so
 // a walk phase is worth more parked lanes.  Scenes without meshes never walk.
-// Bytes of a scene's traversal index as the mesh kernels read it: Node4s, the triangles' DevTri
-// and DevTriShade records and their gate-chain boxes (teapot ~1.4 MB, gopher ~3.7 MB).
-static size_t index_bytes(const HostScene& hs) {
-    return hs.index.nodes.size() * sizeof(Node4) + hs.index.tris.size() * sizeof(DevTri) +
-           hs.st.size() * sizeof(DevTriShade) + hs.index.chain_boxes.size() * sizeof(ChainBox);
-}
-
 static int32_t walk_batch_for(const HostScene& hs) {
     if (!(hs.flags & 1)) return 64;
     return hs.n_tri >= 12000 ? 32 : 28;
@@ -684,11 +677,13 @@ int upload_scene(const HostScene& hs, int device_index, const ptmi_textures* tex
     // 493.6 ms, gopher (C5) 784.2 / 768.2 / 759.6 ms.
     s->dev.walk_batch = walk_batch_for(hs);
     // The hemisphere table in the mesh kernels: the 1-MB (sin, cos) plane shares each XCD's 4-MB L2
-    // with the traversal index.  Round 6, with the path pool, C5 (gopher, index ~3.7 MB) renders in the
-    // same time without it (766.5 / 764.7 against 766.0 / 765.4 ms) and its HBM traffic falls from
-    // 2.25 to 0.76 GB per launch (profiles/r6/hbm1): the table's lines were being evicted and
-    // refetched.  Smaller indexes keep it (before the pool C4 was 2.8 % slower without it).
-    s->dev.hemi_mesh = index_bytes(hs) <= (2u << 20) ? 1 : 0;
+    // with the traversal index.  Round 6, with the path pool, on the gopher (C5, index ~3.7 MB) the
+    // table costs HBM traffic -- 2.1-2.25 GB per launch with it, 0.76 GB without (profiles/r6/hbm1):
+    // its lines are evicted and refetched -- but it still saves time: 753.3 / 754.2 / 755.2 ms with,
+    // 766.7 / 767.7 / 768.3 ms without, alternated on one box (profiles/r6/hm2); the teapot (C4)
+    // 488.5-490.0 with, 503.1 ms without.  At ~3 GB/s the traffic binds nothing, so every mesh scene
+    // reads the table; PTMI_KNOB_HEMI_MESH 0 trades the 1.7 % for the traffic.
+    s->dev.hemi_mesh = 1;
     // (Tests and tuning studies change the plan through ptmi_diag_set_knob; the library reads
     // no tuning variable from the environment.)
     // Mesh scenes: >= 64 samples per chunk.  It binds only on short sample ranges (a rank's

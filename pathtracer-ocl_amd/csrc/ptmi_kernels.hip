@@ -1623,8 +1623,8 @@ __device__ __forceinline__ void hemi_sqrt(float u2, double& r2s, double& rc) {
 #ifndef PTMI_HEMI_TAB_GROUPS
 #define PTMI_HEMI_TAB_GROUPS 1  // mesh scenes read the table too (round 5: with the group kernel's colour
                                 // state in LDS, 2048 spp: C4 594 -> 577, C5 902 -> 897 ms; in round 4 the
-                                // 2 MB table's L2 share had cost C5 ~1.5 % at 512 spp) -- since round 6 only
-                                // where the scene allows it (DevScene::hemi_mesh, ptmi_api.cpp)
+                                // 2 MB table's L2 share had cost C5 ~1.5 % at 512 spp); since round 6 a scene
+                                // switch as well (DevScene::hemi_mesh, ptmi_api.cpp; on by default)
 #endif
 static constexpr int kHemiBits = 16;
 static constexpr int kHemiSize = 1 << kHemiBits;

@@ -277,9 +277,10 @@ def test_whole_tiles_and_chunked_tail(scene, stride):
 
 @pytest.mark.parametrize("scene", ["teapot", "gopher"])
 def test_mesh_hemisphere_table_switch(scene):
-    """The mesh kernels read the hemisphere table only where the scene's index leaves it room in
-    L2 (DevScene::hemi_mesh, ptmi_api.cpp: the teapot yes, the gopher no).  The table holds the
-    bits the kernel computes, so either way the frame is the same, bit for bit."""
+    """The mesh kernels read the hemisphere table unless the scene switches it off
+    (DevScene::hemi_mesh, PTMI_KNOB_HEMI_MESH: a traffic / time trade-off on large meshes).
+    The table holds the bits the kernel computes, so either way the frame is the same, bit
+    for bit."""
     torch, sc = _torch_scene(scene, 64, 48)
     S, n = 40, 64 * 48
     seeds = torch.tensor(layout.seeds_go_float64(n, 21), dtype=torch.float64, device="cuda")
