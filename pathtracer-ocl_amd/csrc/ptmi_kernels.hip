@@ -2543,6 +2543,11 @@ __device__ __forceinline__ void trace_groups_pool(const DevScene& S0, uint32_t s
     acc_lds[0 * kBlock + tid] = 0.0;
     acc_lds[1 * kBlock + tid] = 0.0;
     acc_lds[2 * kBlock + tid] = 0.0;
+    // The lanes read each other's fgi and add into each other's sums from here on: a wave barrier
+    // (one wave per workgroup; LDS serves a wave's operations in program order) keeps the compiler
+    // from moving those accesses across the initialisation, and the one after the loop keeps the
+    // final reads of the sums after every lane's adds.
+    __builtin_amdgcn_wave_barrier();
     // The tile's origin and sample range are the wave's (work_item of lane 0).
     const int tx0 = __builtin_amdgcn_readfirstlane(it.px - (lane & 7));
     const int ty0 = __builtin_amdgcn_readfirstlane(it.py - (lane >> 3));
@@ -2658,6 +2663,7 @@ __device__ __forceinline__ void trace_groups_pool(const DevScene& S0, uint32_t s
             }
         }
     }
+    __builtin_amdgcn_wave_barrier();
     store_sums<PTMI_MESH_PLANES != 0>(work_item<(FL & F_TLIST) != 0>(S0, WP, item, lane), WP, sums, part, acc_lds[0 * kBlock + tid],
                                       acc_lds[1 * kBlock + tid], acc_lds[2 * kBlock + tid]);
 }
@@ -2701,6 +2707,7 @@ __device__ __forceinline__ void trace_flat_pool(const DevScene& S0, uint32_t sam
     acc_lds[0 * kBlock + tid] = 0.0;
     acc_lds[1 * kBlock + tid] = 0.0;
     acc_lds[2 * kBlock + tid] = 0.0;
+    __builtin_amdgcn_wave_barrier();  // (see trace_groups_pool)
     const int tx0 = __builtin_amdgcn_readfirstlane(it.px - (lane & 7));
     const int ty0 = __builtin_amdgcn_readfirstlane(it.py - (lane >> 3));
     const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)it.c0);
@@ -2784,6 +2791,7 @@ __device__ __forceinline__ void trace_flat_pool(const DevScene& S0, uint32_t sam
             }
         }
     }
+    __builtin_amdgcn_wave_barrier();
     store_sums<true>(work_item(S0, WP, blockIdx.x, lane), WP, sums, part, acc_lds[0 * kBlock + tid],
                      acc_lds[1 * kBlock + tid], acc_lds[2 * kBlock + tid]);
 }
